@@ -1,0 +1,175 @@
+/*
+ * rt_hip.h — C-ABI of the MI355X render path (librt_hip.so).
+ *
+ * This is the drop-in boundary that replaces the reference's device entry
+ *   void launch_compute_image_device(vec4* d_pixels, vec4* d_tmpPixels,
+ *        vec4* d_image, const int& width, const int& height,
+ *        const Camera& camera, const vec4* d_lightsPos,
+ *        const vec4* d_lightsColor, const int& nLights,
+ *        const vec4& background, const vec4& ambience, const int& max_depth,
+ *        const Data* data, const BVH::BVHNodes_SoA* bvhNodes);
+ *   (declared mytracer_gpu.h:43-56, defined mytracer_gpu.cu:44-113)
+ * together with the managed-memory scene it reads (struct Data, mydata.h:28-72;
+ * BVH::BVHNodes_SoA, mybvh.h:49-55; allocated by Raytracer::build_Data,
+ * mytracer.cpp:166-296, and BVH::initSoA, mybvh.cpp:375-406).
+ *
+ * Differences by design:
+ *  - the scene is uploaded once with explicit hipMalloc/hipMemcpy into an
+ *    MI355X layout (fp32 2-wide BVH nodes with child boxes in the parent,
+ *    fp64 triangle records in leaf order); no managed memory;
+ *  - the caller passes host SoA arrays (the reference's Data/BVHNodes_SoA
+ *    content, same meaning, packed xyz instead of vec4) and owns the output;
+ *  - errors are returned as status codes with the message in rt_last_error()
+ *    (the reference's CHECK prints and continues, common/common.h:6-15);
+ *  - rows can be restricted / interleaved so one process per GPU renders its
+ *    share of the image (the reference only uses device 0, mytracer_gpu.cu:34).
+ * All pointers are plain; no torch or HIP types appear in the signatures
+ * (streams are passed as void*).
+ */
+#ifndef RT_HIP_H
+#define RT_HIP_H
+
+#include <stddef.h>
+#include "rt_scene.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_OK 0
+#define RT_ERR_INVALID (-1)     /* bad argument / inconsistent scene */
+#define RT_ERR_HIP (-2)         /* HIP runtime failure */
+#define RT_ERR_UNSUPPORTED (-3) /* scene exceeds a compiled limit (e.g. BVH depth) */
+
+#define RT_MAX_LIGHTS 16
+
+/* Host SoA scene: the content of struct Data (mydata.h:28-72) after
+ * BVH::initSoA has permuted the per-triangle arrays into leaf order
+ * (mybvh.cpp:497-503).  Vectors are packed xyz (3 doubles). */
+typedef struct rt_scene_soa {
+  int n_meshes;          /* tMeshCount_ */
+  int n_vertices;        /* tVertexCount_ */
+  int n_vertex_idx;      /* tVertexIdxCount_ = 3 * n_triangles */
+  int n_tex_coords;      /* tTextCoordCount_ */
+  long long n_texels;    /* tTexelCount_ */
+  const int* vertex_mesh_id;     /* [n_vertices]          vertexMeshId_ */
+  const double* vertex_pos;      /* [3*n_vertices]        vertexPos_ */
+  const double* vertex_normals;  /* [3*n_vertices]        vertexNormals_ */
+  const double* face_normals;    /* [3*n_triangles]       normals_ (leaf order) */
+  const int* vertex_idx;         /* [n_vertex_idx]        vertexIdx_ (leaf order, global ids) */
+  const int* texture_idx;        /* [n_vertex_idx]        textureIdx_ (leaf order, global ids) */
+  const double* tex_u;           /* [n_tex_coords]        textureCoordinatesU_ */
+  const double* tex_v;           /* [n_tex_coords]        textureCoordinatesV_ */
+  const unsigned char* texels;   /* [3*n_texels] RGB8     meshTexels_ (vec4 in the reference) */
+  const int* mesh_tex_width;     /* [n_meshes], -1 = none meshTexWidth_ */
+  const int* mesh_tex_height;    /* [n_meshes]            meshTexHeight_ */
+  const long long* mesh_tex_offset; /* [n_meshes]         firstMeshTex_ */
+  const int* mesh_draw_mode;     /* [n_meshes]            meshDrawMode_ */
+  const double* mat_ambient;     /* [3*n_meshes]          materialAmbient_ */
+  const double* mat_diffuse;     /* [3*n_meshes]          materialDiffuse_ */
+  const double* mat_specular;    /* [3*n_meshes]          materialSpecular_ */
+  const double* mat_shininess;   /* [n_meshes]            materialShininess_ */
+  const double* mat_mirror;      /* [n_meshes]            materialMirror_ */
+  const int* mat_shadowable;     /* [n_meshes]            materialShadowable_ */
+} rt_scene_soa;
+
+/* The reference's BVH::BVHNodes_SoA (mybvh.h:49-55), nodes [0, n_nodes). */
+typedef struct rt_bvh_soa {
+  int n_nodes;                 /* nodesUsed_ */
+  const double* bb_min;        /* [3*n_nodes] */
+  const double* bb_max;        /* [3*n_nodes] */
+  const int* left_child;       /* [n_nodes]; right child = left_child + 1 */
+  const int* first_tri;        /* [n_nodes] */
+  const int* tri_count;        /* [n_nodes]; 0 = internal */
+} rt_bvh_soa;
+
+/* Output formats of rt_launch_compute_image. */
+enum {
+  RT_OUT_RGB_F32 = 0,  /* 3 floats per pixel (production) */
+  RT_OUT_RGB_F64 = 1   /* 3 doubles per pixel (parity tests) */
+};
+
+/* Flags of rt_render_params.flags. */
+enum {
+  RT_FLAG_TRAVERSAL_STATS = 1  /* instrumented kernel: counts node visits / triangle tests */
+};
+
+/* One render call.  Rows are rendered as interleaved stripes:
+ * row y is rendered iff row_begin <= y < row_end and
+ * (y / stripe_height) % stripe_count == stripe_index; rendered rows are
+ * packed into the output in increasing y, row-major, pixel (x, y) of local
+ * row r at out[(r*width + x)*3 + c] (the reference's pixels[y*W+x],
+ * mytracer_gpu.cu:158).  stripe_count == 1 renders every row in range. */
+typedef struct rt_render_params {
+  rt_camera camera;
+  int n_lights;                          /* <= RT_MAX_LIGHTS */
+  int max_depth;                         /* reflection bounces after the primary hit */
+  rt_light lights[RT_MAX_LIGHTS];
+  double background[3];
+  double ambience[3];
+  int spp_n;            /* n: n*n stratified samples per pixel (mytracer_gpu.cu:202-221); 1 = one ray through (x,y) */
+  int row_begin;
+  int row_end;          /* <= 0 means camera.height */
+  int stripe_height;    /* >= 1 */
+  int stripe_count;     /* >= 1 */
+  int stripe_index;     /* [0, stripe_count) */
+  int out_format;       /* RT_OUT_* */
+  int flags;            /* RT_FLAG_* */
+} rt_render_params;
+
+/* Ray counters of one launch (canonical definition: DESIGN.md §5).
+ * primary = pixels*spp; shadow = shading points x lights with a shadowable
+ * material (mytracer.cpp:589); reflection = shading points with mirror > 0
+ * below max_depth (mytracer.cpp:547).  node_visits / tri_tests / hits are
+ * filled only with RT_FLAG_TRAVERSAL_STATS. */
+typedef struct rt_stats {
+  long long primary_rays;
+  long long shadow_rays;
+  long long reflection_rays;
+  long long node_visits;      /* fp32 2-wide nodes fetched (= internal-node pops) */
+  long long tri_tests;        /* triangle records tested */
+  long long closest_hits;     /* closest-hit rays that hit (shading fetches) */
+  long long pixels;           /* pixels written */
+  long long reserved_;
+} rt_stats;
+
+typedef struct rt_scene rt_scene;   /* opaque device-resident scene */
+
+/* Uploads the scene to HIP device `device` (hipSetDevice), converting the
+ * host SoA + reference BVH into the MI355X layout.  Leaves the device current. */
+int rt_scene_upload(const rt_scene_soa* soa, const rt_bvh_soa* bvh, int device, rt_scene** out);
+
+/* Device bytes held by the scene (nodes, triangles, shading data). */
+long long rt_scene_device_bytes(const rt_scene* scene);
+
+/* Number of rows rt_launch_compute_image writes for these params. */
+int rt_rows_in_shard(const rt_render_params* p);
+
+/* Renders into the caller-owned DEVICE buffer d_out (rows x width x 3 of the
+ * chosen format) on `stream` (hipStream_t, NULL = the null stream).
+ * Asynchronous unless stats != NULL, in which case it synchronises the stream
+ * and fills *stats.  Replaces launch_compute_image_device's primary pass
+ * (mytracer_gpu.cu:66-81); the adaptive pass (:83-109) is SURVEY §8f "next". */
+int rt_launch_compute_image(rt_scene* scene, const rt_render_params* p, void* d_out,
+                            rt_stats* stats, void* stream);
+
+/* Convenience for tests / CLI: renders into a HOST buffer (allocates a device
+ * buffer internally, synchronous). */
+int rt_render_to_host(rt_scene* scene, const rt_render_params* p, void* host_out, rt_stats* stats);
+
+/* Milliseconds of the last launch on this scene, measured with hipEvents
+ * recorded around the kernel on its stream (valid after the stream syncs). */
+int rt_last_kernel_ms(rt_scene* scene, float* ms);
+
+void rt_scene_free(rt_scene* scene);
+
+/* Thread-local message of the last failing call. */
+const char* rt_last_error(void);
+
+/* Build info string (kernel variants, arch) for logs. */
+const char* rt_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_HIP_H */

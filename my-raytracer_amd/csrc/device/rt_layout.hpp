@@ -1,0 +1,71 @@
+// rt_layout.hpp — device-resident scene layout of the MI355X render path.
+//
+// Replaces the reference's managed-memory struct Data (mydata.h:28-72) and
+// BVH::BVHNodes_SoA (mybvh.h:49-55) for the traversal loop:
+//
+//  * GNode (64 B = half a 128-B line): one INTERNAL node of the reference's
+//    median-split tree holding the boxes of its two children (the reference
+//    re-reads 5 SoA arrays per pop, mytracer_gpu.cu:360-364, then 2 child
+//    boxes, :397-403).  Boxes are fp32, rounded outward and grown by
+//    delta = 2^-20 * max|vertex| so the fp32 slab test is conservative for
+//    the fp64 ray.  Per axis one float4 {lo0, hi0, lo1, hi1}
+//    so one dwordx4 load feeds both children's slab on that axis.  Nodes are
+//    numbered in depth-first preorder (left child = parent + 1).
+//    ref: internal child -> its GNode index; leaf child -> LEAF | first slot;
+//    EMPTY marks the absent sibling of a single-leaf root.
+//  * GTri (80 B): fp64 triangle record in leaf order, holding exactly the
+//    operands of the reference's Cramer test (mymesh.cpp:190-193):
+//    e1 = p0 - p2, e2 = p1 - p2, p2, plus mesh id and an end-of-leaf flag.
+//  * Shading data is only touched once per closest hit: per-slot vertex /
+//    uv indices, face normals, vertex normals, uvs, texels, materials.
+#pragma once
+#include <cstdint>
+
+namespace rtk {
+
+constexpr uint32_t kLeaf = 0x80000000u;
+constexpr uint32_t kEmpty = 0x7fffffffu;
+constexpr uint32_t kDone = 0xffffffffu;
+constexpr int kNoHit = 0x7fffffff;
+
+struct alignas(64) GNode {
+  float x[4];   // lo0, hi0, lo1, hi1
+  float y[4];
+  float z[4];
+  uint32_t ref[2];
+  uint32_t pad[2];
+};
+static_assert(sizeof(GNode) == 64, "GNode must be 64 bytes");
+
+struct alignas(16) GTri {
+  double e1[3];
+  double e2[3];
+  double p2[3];
+  int32_t mesh;
+  uint32_t last;   // 1 = last triangle of its leaf
+};
+static_assert(sizeof(GTri) == 80, "GTri must be 80 bytes");
+
+struct alignas(16) TriShade {
+  int32_t v[3];    // global vertex ids (vertexIdx_)
+  int32_t t[3];    // global uv ids (textureIdx_), -1 = none
+  int32_t pad[2];
+};
+static_assert(sizeof(TriShade) == 32, "TriShade must be 32 bytes");
+
+struct alignas(16) GMat {
+  double ka[3];
+  double kd[3];
+  double ks[3];
+  double shininess;
+  double mirror;
+  int32_t shadowable;
+  int32_t draw_mode;
+  int32_t tex_w;    // -1: none
+  int32_t tex_h;
+  int64_t tex_off;  // texel offset
+  int64_t pad;
+};
+static_assert(sizeof(GMat) == 128, "GMat must be 128 bytes");
+
+}  // namespace rtk

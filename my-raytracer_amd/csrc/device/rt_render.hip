@@ -1,0 +1,1020 @@
+// rt_render.hip — the MI355X render path: one flattened, persistent CDNA4
+// kernel plus the C-ABI boundary of librt_hip.so (include/rt_hip.h).
+//
+// Replaces the reference's device chain (mytracer_gpu.cu:119-693)
+//   compute_image_device -> trace_device -> intersect_scene_device ->
+//   intersectBVH_device -> intersect_triangle_device / intersectAABB_device
+//   -> lighting_device (+ diffuse_device, reflection_device)
+// with ONE kernel in which every lane runs a small state machine over the
+// rays of its pixel (primary -> per-light shadow rays -> reflection -> ...),
+// all ray kinds sharing one traversal loop:
+//   * traversal: ordered, t-culled, 2-wide fp32 nodes (rt_layout.hpp), the
+//     per-ray stack in LDS ([entry][thread], bank-conflict free), while-while
+//     loop; closest-hit for primary / reflection rays, any-hit bounded by the
+//     light distance for shadow rays (the reference traces full closest-hit
+//     shadow rays, mytracer_gpu.cu:653-660; the shadow predicate is the same);
+//   * triangle test and all shading in fp64 with the reference CPU
+//     renderer's operation order (mymesh.cpp:186-235, mytracer.cpp:510-608),
+//     compiled with fp-contract off, so hits are bit-identical to the oracle;
+//   * work distribution: persistent workgroups pull 8x8 pixel tiles from 8
+//     work heads, one per XCD group (blockIdx % 8), refilled per wave with a
+//     single atomic when >= kRefill lanes are idle (__ballot + mbcnt), which
+//     keeps lanes busy despite divergent ray lengths;
+//   * reflection rays are spawned only when mirror > 0 (CPU semantics,
+//     mytracer.cpp:547); the reference GPU traces max_depth zero-weight
+//     bounces (mytracer_gpu.cu:281-310) — same pixels, less work.
+// No MFMA: the path is a traversal / latency problem.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../../include/rt_hip.h"
+#include "rt_layout.hpp"
+
+#pragma clang fp contract(off)
+
+using namespace rtk;
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kGroups = 8;          // work heads (XCD groups)
+constexpr int kRefill = 16;         // refill a wave when this many lanes are idle
+constexpr int kCtrWords = 16;       // [0,8) work heads, [8,16) stats
+
+enum : int { ST_FETCH = 0, ST_CLOSEST = 1, ST_SHADOW = 2, ST_DONE = 3 };
+enum : int { CS_PRIMARY = 8, CS_SHADOW, CS_REFLECT, CS_NODES, CS_TRIS, CS_HITS, CS_PIXELS };
+
+struct KParams {
+  const GNode* nodes;
+  const GTri* tris;
+  const TriShade* shade;
+  const double* fnorm;
+  const double* vnorm;
+  const double* tu;
+  const double* tv;
+  const unsigned char* texels;
+  const GMat* mats;
+  unsigned long long* ctr;
+  double* pstate;       // [kFields][nslots] path state
+  const double* lights; // [n_lights][6] position xyz, colour rgb
+  void* out;
+  size_t nslots;
+  int n_gnodes;
+  int out_fmt;
+  int pad0[2];
+  double root_lo[3], root_hi[3];
+  double eye[3], ll[3], xd[3], yd[3];
+  int W, H;
+  int n_lights, max_depth;
+  double bg[3], amb[3];
+  int spp_n;
+  int row_begin, stripe_h, stripe_count, stripe_index;
+  int rows;
+  int tiles_x;
+  int pad1;
+  long long n_tiles;
+};
+
+// ---- fp64 vector ops (course vec4 semantics on xyz) ----
+struct D3 {
+  double x, y, z;
+};
+__device__ __forceinline__ D3 d3(double x, double y, double z) { return D3{x, y, z}; }
+__device__ __forceinline__ D3 add(D3 a, D3 b) { return D3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ D3 sub(D3 a, D3 b) { return D3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ D3 scl(double s, D3 a) { return D3{s * a.x, s * a.y, s * a.z}; }
+__device__ __forceinline__ D3 mul(D3 a, D3 b) { return D3{a.x * b.x, a.y * b.y, a.z * b.z}; }
+__device__ __forceinline__ double dot(D3 a, D3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ D3 normalize(D3 v) {
+  const double n = sqrt(dot(v, v));
+  if (n > 0.0) return D3{v.x / n, v.y / n, v.z / n};
+  return v;
+}
+__device__ __forceinline__ double stdmax(double a, double b) { return (a < b) ? b : a; }
+__device__ __forceinline__ double stdmin(double a, double b) { return (b < a) ? b : a; }
+
+// det4D_device (myutils_gpu.h:33-37) / det4D (myutils.cpp:47-51).
+__device__ __forceinline__ double det3(D3 v1, D3 v2, D3 v3) {
+  return v1.x * (v2.y * v3.z - v3.y * v2.z) - v2.x * (v1.y * v3.z - v3.y * v1.z) +
+         v3.x * (v1.y * v2.z - v2.y * v1.z);
+}
+
+__device__ __forceinline__ float next_up(float f) {
+  if (f != f || f == INFINITY) return f;
+  if (f == 0.0f) return __uint_as_float(1u);
+  const uint32_t u = __float_as_uint(f);
+  return __uint_as_float(f > 0.0f ? u + 1u : u - 1u);
+}
+__device__ __forceinline__ float next_down(float f) {
+  if (f != f || f == -INFINITY) return f;
+  if (f == 0.0f) return __uint_as_float(0x80000001u);
+  const uint32_t u = __float_as_uint(f);
+  return __uint_as_float(f > 0.0f ? u - 1u : u + 1u);
+}
+__device__ __forceinline__ float round_up_f(double x) {
+  float f = (float)x;
+  if ((double)f < x) f = next_up(f);
+  return f;
+}
+__device__ __forceinline__ float round_down_f(double x) {
+  float f = (float)x;
+  if ((double)f > x) f = next_down(f);
+  return f;
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+  return v;
+}
+
+struct TriOps {
+  D3 e1, e2, p2;
+  int mesh;
+  uint32_t last;
+};
+__device__ __forceinline__ TriOps load_tri(const GTri* tris, uint32_t i) {
+  const double2* q = reinterpret_cast<const double2*>(tris + i);
+  const double2 a = q[0], b = q[1], c = q[2], d = q[3], e = q[4];
+  TriOps T;
+  T.e1 = d3(a.x, a.y, b.x);
+  T.e2 = d3(b.y, c.x, c.y);
+  T.p2 = d3(d.x, d.y, e.x);
+  const int2 meta = *reinterpret_cast<const int2*>(&q[4].y);
+  T.mesh = meta.x;
+  T.last = (uint32_t)meta.y;
+  return T;
+}
+
+// Path-state fields kept in global memory, one 224-B record per lane of the
+// persistent grid.  They are touched only when a ray completes.
+enum : int {
+  F_PCOL = 0, F_SCOL = 3, F_W = 6, F_HP = 7, F_HN = 10, F_HVIEW = 13, F_HDIFF = 16,
+  F_LACC = 19, F_CONTRIB = 22, F_MIRROR = 25, kFields = 28
+};
+
+// LDS ray slots ([field][thread], conflict-free): the only hand-over between
+// the shading phase (writes the next ray) and the traversal phase (reads it).
+struct RaySlots {
+  double* o[3];
+  double* d[3];
+  double* tlim;
+};
+
+// Per-wave loop, two phases:
+//   TRAVERSE: every busy lane loads its ray from LDS, sets up the fp32 box
+//             ray and runs ordered traversal until ALL lanes of the wave are
+//             done (while-while); only (best, t, shadow flag) survive.
+//   SHADE:    lanes whose ray finished run the pixel's state machine from the
+//             global path state and write their next ray (if any) to LDS.
+// Nothing but a few ids is live across the phase boundary, which keeps the
+// kernel at 4 waves/SIMD despite fp64 shading.
+template <bool STATS>
+__global__ void __launch_bounds__(kBlock, 4) render_kernel(KParams P) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  double* lds_d = reinterpret_cast<double*>(lds_raw);
+  RaySlots R;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    R.o[k] = lds_d + k * kBlock + threadIdx.x;
+    R.d[k] = lds_d + (3 + k) * kBlock + threadIdx.x;
+  }
+  R.tlim = lds_d + 6 * kBlock + threadIdx.x;
+  uint32_t* stk = reinterpret_cast<uint32_t*>(lds_raw + 7 * kBlock * sizeof(double)) + threadIdx.x;
+
+  const int lane = threadIdx.x & 63;
+  const unsigned long long lane_below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  double* ps = P.pstate + ((size_t)blockIdx.x * kBlock + threadIdx.x) * kFields;
+  auto LD = [&](int f) { return ps[f]; };
+  auto ST = [&](int f, double v) { ps[f] = v; };
+  auto LD3 = [&](int f) { return d3(ps[f], ps[f + 1], ps[f + 2]); };
+  auto ST3 = [&](int f, D3 v) { ps[f] = v.x; ps[f + 1] = v.y; ps[f + 2] = v.z; };
+
+  // wave-uniform work-head cursor
+  int head = blockIdx.x % kGroups;
+  int heads_left = kGroups;
+
+  // ---- per-lane state live across phases ----
+  int state = ST_FETCH;
+  int px = 0, lrow = 0, py = 0, sample = 0, depth = 0, light = 0, mesh = 0;
+  int best = kNoHit;
+  double thit = DBL_MAX;
+  bool shadow_hit = false;
+  unsigned c_primary = 0, c_shadow = 0, c_refl = 0, c_hits = 0;
+  unsigned long long c_nodes = 0, c_tris = 0;
+
+  // Ray(o, d): stores origin, normalised direction and t-limit to the LDS slot.
+  auto emit_ray = [&](D3 o, D3 dir, double t_limit) {
+    const D3 d = normalize(dir);
+    *R.o[0] = o.x; *R.o[1] = o.y; *R.o[2] = o.z;
+    *R.d[0] = d.x; *R.d[1] = d.y; *R.d[2] = d.z;
+    *R.tlim = t_limit;
+  };
+
+  // primary ray of the current sample (mytracer_gpu.cu:202-209; Camera::primary_ray)
+  auto start_sample = [&]() {
+    const int n = P.spp_n;
+    const int si = sample / n, sj = sample - si * n;
+    const double xo = (si) / (double)n - 0.5 + 1.0 / (2.0 * n);
+    const double yo = (sj) / (double)n - 0.5 + 1.0 / (2.0 * n);
+    const double X = (double)px + xo, Y = (double)py + yo;
+    const D3 dir = d3(P.ll[0] + X * P.xd[0] + Y * P.yd[0] - P.eye[0],
+                      P.ll[1] + X * P.xd[1] + Y * P.yd[1] - P.eye[1],
+                      P.ll[2] + X * P.xd[2] + Y * P.yd[2] - P.eye[2]);
+    ST3(F_SCOL, d3(0, 0, 0));
+    ST(F_W, 1.0);
+    depth = 0;
+    c_primary++;
+    emit_ray(d3(P.eye[0], P.eye[1], P.eye[2]), dir, DBL_MAX);
+    state = ST_CLOSEST;
+  };
+
+  for (;;) {
+    // ---------------- refill idle lanes (one atomic per wave) ----------------
+    unsigned long long m_fetch = __ballot(state == ST_FETCH);
+    unsigned long long m_busy = __ballot(state == ST_CLOSEST || state == ST_SHADOW);
+    while (m_fetch && (__popcll(m_fetch) >= kRefill || m_busy == 0) && heads_left > 0) {
+      const long long g0 = (P.n_tiles * head / kGroups) * 64;
+      const long long g1 = (P.n_tiles * (head + 1) / kGroups) * 64;
+      const int cnt = __popcll(m_fetch);
+      const int leader = __ffsll((long long)m_fetch) - 1;
+      unsigned long long base = 0;
+      if (lane == leader) base = atomicAdd(&P.ctr[head], (unsigned long long)cnt);
+      base = __shfl(base, leader);
+      const long long start = g0 + (long long)base;
+      if (start >= g1) {   // head exhausted: move to the next XCD group's range
+        head = (head + 1) % kGroups;
+        heads_left--;
+        continue;
+      }
+      if (state == ST_FETCH) {
+        const long long wk = start + __popcll(m_fetch & lane_below);
+        if (wk < g1) {
+          const long long tile = wk >> 6;
+          const int j = (int)(wk & 63);
+          const long long ty = tile / P.tiles_x;
+          const int tx = (int)(tile - ty * P.tiles_x);
+          px = tx * 8 + (j & 7);
+          lrow = (int)ty * 8 + (j >> 3);
+          if (px < P.W && lrow < P.rows) {
+            py = (P.stripe_count == 1)
+                     ? P.row_begin + lrow
+                     : ((lrow / P.stripe_h) * P.stripe_count + P.stripe_index) * P.stripe_h + (lrow % P.stripe_h);
+            sample = 0;
+            ST3(F_PCOL, d3(0, 0, 0));
+            start_sample();
+          }
+        }
+      }
+      m_fetch = __ballot(state == ST_FETCH);
+      m_busy = __ballot(state == ST_CLOSEST || state == ST_SHADOW);
+      if (__popcll(m_fetch) < kRefill && m_busy != 0) break;
+    }
+    if (heads_left == 0 && state == ST_FETCH) state = ST_DONE;
+    const bool busy = (state == ST_CLOSEST || state == ST_SHADOW);
+    if (__ballot(busy) == 0) {
+      if (__ballot(state != ST_DONE) == 0) break;
+      continue;
+    }
+
+    // ================= TRAVERSE phase =================
+    {
+      const bool anyhit = (state == ST_SHADOW);
+      const D3 ro = d3(*R.o[0], *R.o[1], *R.o[2]);
+      const D3 rd = d3(*R.d[0], *R.d[1], *R.d[2]);
+      double tlim = *R.tlim;
+      best = kNoHit;
+      shadow_hit = false;
+      uint32_t cur = kDone;
+      double t_off = 0.0;
+      if (busy && P.n_gnodes > 0) {   // conservative fp32 box ray (oracle/rt_oracle.c gray_setup)
+        bool miss = false;
+        const double o3[3] = {ro.x, ro.y, ro.z}, d3v[3] = {rd.x, rd.y, rd.z};
+        bool inside = true;
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+          if (!(o3[k] >= P.root_lo[k] && o3[k] <= P.root_hi[k])) inside = false;
+        if (!inside) {
+          double tn = -DBL_MAX, tf = DBL_MAX;
+#pragma unroll
+          for (int k = 0; k < 3; ++k) {
+            if (d3v[k] == 0.0) {
+              if (o3[k] < P.root_lo[k] || o3[k] > P.root_hi[k]) miss = true;
+              continue;
+            }
+            double t0 = (P.root_lo[k] - o3[k]) / d3v[k];
+            double t1 = (P.root_hi[k] - o3[k]) / d3v[k];
+            if (t0 > t1) { const double t = t0; t0 = t1; t1 = t; }
+            if (t0 > tn) tn = t0;
+            if (t1 < tf) tf = t1;
+          }
+          if (tn > tf || tf < 0.0) miss = true;
+          t_off = tn > 0.0 ? tn : 0.0;
+        }
+        if (miss) t_off = 0.0;
+        else cur = 0;
+      }
+      float inv[3];
+      {
+        const double d3v[3] = {rd.x, rd.y, rd.z};
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          float df = (float)d3v[k];
+          if (fabsf(df) < 1e-20f) df = signbit(d3v[k]) ? -1e-20f : 1e-20f;
+          inv[k] = 1.0f / df;
+        }
+      }
+      const float ofx = (float)(ro.x + t_off * rd.x);
+      const float ofy = (float)(ro.y + t_off * rd.y);
+      const float ofz = (float)(ro.z + t_off * rd.z);
+      const float ivx = inv[0], ivy = inv[1], ivz = inv[2];
+      const float lo_c = round_down_f(-t_off);
+      float hi_c = round_up_f(tlim - t_off);
+      int sp = 0;
+      const D3 c3 = d3(-rd.x, -rd.y, -rd.z);
+
+      while (__ballot(cur != kDone) != 0) {
+        while (!(cur & kLeaf)) {   // internal node (kDone carries the leaf bit)
+          if (STATS) c_nodes++;
+          const float4* nq = reinterpret_cast<const float4*>(P.nodes + cur);
+          const float4 bx = nq[0], by = nq[1], bz = nq[2];
+          const uint2 rf = *reinterpret_cast<const uint2*>(nq + 3);
+          const float ax0 = (bx.x - ofx) * ivx, ax1 = (bx.y - ofx) * ivx;
+          const float ay0 = (by.x - ofy) * ivy, ay1 = (by.y - ofy) * ivy;
+          const float az0 = (bz.x - ofz) * ivz, az1 = (bz.y - ofz) * ivz;
+          const float bx0 = (bx.z - ofx) * ivx, bx1 = (bx.w - ofx) * ivx;
+          const float by0 = (by.z - ofy) * ivy, by1 = (by.w - ofy) * ivy;
+          const float bz0 = (bz.z - ofz) * ivz, bz1 = (bz.w - ofz) * ivz;
+          const float tn0 = fmaxf(fmaxf(fminf(ax0, ax1), fminf(ay0, ay1)), fmaxf(fminf(az0, az1), lo_c));
+          const float tf0 = fminf(fminf(fmaxf(ax0, ax1), fmaxf(ay0, ay1)), fminf(fmaxf(az0, az1), hi_c));
+          const float tn1 = fmaxf(fmaxf(fminf(bx0, bx1), fminf(by0, by1)), fmaxf(fminf(bz0, bz1), lo_c));
+          const float tf1 = fminf(fminf(fmaxf(bx0, bx1), fmaxf(by0, by1)), fminf(fmaxf(bz0, bz1), hi_c));
+          const bool h0 = tn0 <= tf0;
+          const bool h1 = (tn1 <= tf1) && (rf.y != kEmpty);
+          if (h0 && h1) {
+            const bool swap = tn1 < tn0;
+            stk[sp * kBlock] = swap ? rf.x : rf.y;
+            sp++;
+            cur = swap ? rf.y : rf.x;
+          } else if (h0) {
+            cur = rf.x;
+          } else if (h1) {
+            cur = rf.y;
+          } else {
+            cur = (sp > 0) ? stk[--sp * kBlock] : kDone;
+          }
+        }
+        if (cur != kDone) {   // leaf: test its triangles in slot order
+          uint32_t i = cur & ~kLeaf;
+          for (;;) {
+            if (STATS) c_tris++;
+            const TriOps T = load_tri(P.tris, i);
+            // Mesh::intersect_triangle (mymesh.cpp:190-215), same values, early-outs reordered
+            const D3 c4 = sub(ro, T.p2);
+            const double S = det3(T.e1, T.e2, c3);
+            if (fabs(S) >= 1e-10) {
+              const double t = det3(T.e1, T.e2, c4) / S;
+              const bool cand = anyhit ? (t < tlim) : (t <= tlim);
+              if (t > 1e-5 && cand) {
+                const double alpha = det3(c4, T.e2, c3) / S;
+                const double beta = det3(T.e1, c4, c3) / S;
+                const double gamma = (1.0 - alpha - beta);
+                const bool inside = (0.0 <= alpha && alpha <= 1.0) && (0.0 <= beta && beta <= 1.0) &&
+                                    (0.0 <= gamma && gamma <= 1.0);
+                if (inside) {
+                  if (anyhit) {
+                    shadow_hit = true;
+                    cur = kDone;
+                    break;
+                  }
+                  if (t < tlim || (int)i < best) {   // ties: smallest slot (mybvh.cpp:169 visit order)
+                    tlim = t;
+                    best = (int)i;
+                    hi_c = round_up_f(tlim - t_off);
+                  }
+                }
+              }
+            }
+            if (T.last) break;
+            ++i;
+          }
+          if (cur != kDone) cur = (sp > 0) ? stk[--sp * kBlock] : kDone;
+        }
+      }
+      thit = tlim;
+    }
+    asm volatile("" ::: "memory");
+
+    // ================= SHADE phase =================
+    if (busy) {
+      bool lights_phase = false, fresh_hit = false, finish = false;
+      D3 hp = d3(0, 0, 0), hn = d3(0, 0, 0), hview = d3(0, 0, 0), hdiff = d3(0, 0, 0), lacc = d3(0, 0, 0);
+      double mirror = 0.0;
+      if (state == ST_CLOSEST) {
+        if (best == kNoHit) {   // miss: background (mytracer_gpu.cu:262, :292)
+          ST3(F_SCOL, add(LD3(F_SCOL), scl(LD(F_W), d3(P.bg[0], P.bg[1], P.bg[2]))));
+          finish = true;
+        } else {
+          if (STATS) c_hits++;
+          // hit attributes: mymesh.cpp:217-235 (texture :70-95)
+          const D3 ro = d3(*R.o[0], *R.o[1], *R.o[2]);
+          const D3 rd = d3(*R.d[0], *R.d[1], *R.d[2]);
+          const TriOps T = load_tri(P.tris, (uint32_t)best);
+          const D3 c3 = d3(-rd.x, -rd.y, -rd.z);
+          const D3 c4 = sub(ro, T.p2);
+          const double S = det3(T.e1, T.e2, c3);
+          const double alpha = det3(c4, T.e2, c3) / S;
+          const double beta = det3(T.e1, c4, c3) / S;
+          const double gamma = (1.0 - alpha - beta);
+          hp = add(ro, scl(thit, rd));
+          hview = c3;
+          mesh = T.mesh;
+          const GMat& M = P.mats[mesh];
+          mirror = M.mirror;
+          if (M.draw_mode == RT_DRAW_FLAT) {
+            const double* fnp = P.fnorm + 3 * (size_t)best;
+            hn = d3(fnp[0], fnp[1], fnp[2]);
+          } else {
+            const TriShade sh = P.shade[best];
+            const double* n0 = P.vnorm + 3 * (size_t)sh.v[0];
+            const double* n1 = P.vnorm + 3 * (size_t)sh.v[1];
+            const double* n2 = P.vnorm + 3 * (size_t)sh.v[2];
+            hn = d3(alpha * n0[0] + beta * n1[0] + gamma * n2[0], alpha * n0[1] + beta * n1[1] + gamma * n2[1],
+                    alpha * n0[2] + beta * n1[2] + gamma * n2[2]);
+          }
+          if (M.tex_w > 0) {
+            const TriShade sh = P.shade[best];
+            double u = alpha * P.tu[sh.t[0]] + beta * P.tu[sh.t[1]] + gamma * P.tu[sh.t[2]];
+            double v = alpha * P.tv[sh.t[0]] + beta * P.tv[sh.t[1]] + gamma * P.tv[sh.t[2]];
+            u = u < 0.0 ? 0.0 : (1.0 < u ? 1.0 : u);
+            v = v < 0.0 ? 0.0 : (1.0 < v ? 1.0 : v);
+            const unsigned TW = (unsigned)M.tex_w, TH = (unsigned)M.tex_h;
+            const int tx = (int)round(u * (TW - 1));
+            const int ty = (int)round((1.0 - v) * (TH - 1));
+            const unsigned char* t3 = P.texels + 3 * (M.tex_off + (long long)ty * TW + tx);
+            hdiff = d3((double)t3[0] / 255.0, (double)t3[1] / 255.0, (double)t3[2] / 255.0);
+          } else {
+            hdiff = d3(M.kd[0], M.kd[1], M.kd[2]);
+          }
+          // ambient term (mytracer.cpp:574-576)
+          lacc = d3(0.0 + P.amb[0] * M.ka[0], 0.0 + P.amb[1] * M.ka[1], 0.0 + P.amb[2] * M.ka[2]);
+          light = 0;
+          lights_phase = true;
+          fresh_hit = true;
+        }
+      } else {   // shadow ray of light `light` finished (mytracer.cpp:599-605)
+        lacc = LD3(F_LACC);
+        if (!shadow_hit) lacc = add(lacc, LD3(F_CONTRIB));
+        light++;
+        hp = LD3(F_HP); hn = LD3(F_HN); hview = LD3(F_HVIEW); hdiff = LD3(F_HDIFF);
+        mirror = LD(F_MIRROR);
+        lights_phase = true;
+      }
+      if (lights_phase) {
+        const GMat& M = P.mats[mesh];
+        bool launched = false;
+        while (light < P.n_lights) {   // mytracer.cpp:579-606
+          const double* L6 = P.lights + 6 * light;
+          const D3 to_l = sub(d3(L6[0], L6[1], L6[2]), hp);
+          const D3 l = normalize(to_l);
+          const double diff = stdmax(0.0, dot(hn, l));
+          double refl = 0.0;
+          if (diff > 0.0) {   // reflection(), mytracer.cpp:524-534
+            const double s = 2.0 * dot(hn, l);
+            const D3 r = normalize(sub(scl(s, hn), l));
+            refl = stdmax(0.0, dot(r, hview));
+          }
+          refl = pow(refl, M.shininess);
+          const D3 contrib = d3(L6[3] * (hdiff.x * diff + M.ks[0] * refl), L6[4] * (hdiff.y * diff + M.ks[1] * refl),
+                                L6[5] * (hdiff.z * diff + M.ks[2] * refl));
+          if (M.shadowable) {   // shadow ray, mytracer.cpp:589-600
+            if (fresh_hit) {
+              ST3(F_HP, hp); ST3(F_HN, hn); ST3(F_HVIEW, hview); ST3(F_HDIFF, hdiff);
+              ST(F_MIRROR, mirror);
+            }
+            ST3(F_LACC, lacc);
+            ST3(F_CONTRIB, contrib);
+            c_shadow++;
+            emit_ray(add(hp, scl(1e-4, l)), l, sqrt(dot(to_l, to_l)));
+            state = ST_SHADOW;
+            launched = true;
+            break;
+          }
+          lacc = add(lacc, contrib);
+          light++;
+        }
+        if (!launched) {
+          // all lights done; reflect only if mirror > 0 (subtrace, mytracer.cpp:546-555)
+          const double w = LD(F_W);
+          ST3(F_SCOL, add(LD3(F_SCOL), scl(w, scl(1.0 - mirror, lacc))));
+          if (mirror > 0.0 && depth < P.max_depth) {
+            ST(F_W, w * mirror);
+            depth++;
+            const D3 d = d3(-hview.x, -hview.y, -hview.z);   // direction of the ray that hit
+            const double s = 2.0 * dot(hn, d);               // reflect(d, n) = d - 2(n.d)n
+            const D3 v = sub(d, scl(s, hn));
+            c_refl++;
+            emit_ray(add(hp, scl(1e-4, v)), v, DBL_MAX);
+            state = ST_CLOSEST;
+          } else {
+            finish = true;
+          }
+        }
+      }
+      if (finish) {
+        const D3 pcol = add(LD3(F_PCOL), LD3(F_SCOL));
+        sample++;
+        if (sample < P.spp_n * P.spp_n) {
+          ST3(F_PCOL, pcol);
+          start_sample();
+        } else {   // compute_image: average, clamp, store (mytracer_gpu.cu:155-159, 221-227)
+          const double nn = (double)(P.spp_n * P.spp_n);
+          const double r = stdmin(pcol.x / nn, 1.0), g = stdmin(pcol.y / nn, 1.0), b = stdmin(pcol.z / nn, 1.0);
+          const size_t o = 3 * ((size_t)lrow * P.W + px);
+          if (P.out_fmt == RT_OUT_RGB_F64) {
+            double* out = reinterpret_cast<double*>(P.out) + o;
+            out[0] = r; out[1] = g; out[2] = b;
+          } else {
+            float* out = reinterpret_cast<float*>(P.out) + o;
+            out[0] = (float)r; out[1] = (float)g; out[2] = (float)b;
+          }
+          state = ST_FETCH;
+        }
+      }
+    }
+    asm volatile("" ::: "memory");
+  }
+
+  // ---------------- counters: one atomic per wave and counter ----------------
+  const unsigned long long s0 = wave_sum(c_primary), s1 = wave_sum(c_shadow), s2 = wave_sum(c_refl);
+  unsigned long long s3 = 0, s4 = 0, s5 = 0;
+  if (STATS) { s3 = wave_sum(c_nodes); s4 = wave_sum(c_tris); s5 = wave_sum(c_hits); }
+  if (lane == 0) {
+    atomicAdd(&P.ctr[CS_PRIMARY], s0);
+    atomicAdd(&P.ctr[CS_SHADOW], s1);
+    atomicAdd(&P.ctr[CS_REFLECT], s2);
+    if (STATS) {
+      atomicAdd(&P.ctr[CS_NODES], s3);
+      atomicAdd(&P.ctr[CS_TRIS], s4);
+      atomicAdd(&P.ctr[CS_HITS], s5);
+    }
+  }
+}
+
+// ===========================================================================
+// host side
+// ===========================================================================
+thread_local std::string g_error;
+
+int fail(int code, const std::string& msg) {
+  g_error = msg;
+  return code;
+}
+
+#define HIP_TRY(call)                                                                          \
+  do {                                                                                         \
+    const hipError_t e_ = (call);                                                              \
+    if (e_ != hipSuccess)                                                                      \
+      return fail(RT_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_));              \
+  } while (0)
+
+float round_down_host(double x) {
+  float f = (float)x;
+  if ((double)f > x) f = std::nextafterf(f, -INFINITY);
+  return f;
+}
+float round_up_host(double x) {
+  float f = (float)x;
+  if ((double)f < x) f = std::nextafterf(f, INFINITY);
+  return f;
+}
+
+using KernelFn = void (*)(KParams);
+
+struct Variant {
+  KernelFn fn;
+  bool stats;
+};
+
+const Variant kVariants[] = {
+    {render_kernel<false>, false},
+    {render_kernel<true>, true},
+};
+constexpr int kNumVariants = 2;
+constexpr int kMaxDepth = 128;   // LDS stack: depth * 256 threads * 4 B <= 128 KiB
+// LDS per block: 7 doubles of ray slot + stack_words u32 per thread.
+size_t lds_bytes(int stack_words) { return (size_t)kBlock * (7 * sizeof(double) + (size_t)stack_words * sizeof(uint32_t)); }
+
+}  // namespace
+
+struct rt_scene {
+  int device = 0;
+  GNode* d_nodes = nullptr;
+  GTri* d_tris = nullptr;
+  TriShade* d_shade = nullptr;
+  double* d_fnorm = nullptr;
+  double* d_vnorm = nullptr;
+  double* d_tu = nullptr;
+  double* d_tv = nullptr;
+  unsigned char* d_texels = nullptr;
+  GMat* d_mats = nullptr;
+  unsigned long long* d_ctr = nullptr;
+  int n_gnodes = 0;
+  long long n_tris = 0;
+  int n_meshes = 0;
+  int depth = 0;
+  int stack_words = 1;          // LDS stack entries per thread (>= tree depth)
+  double* d_pstate = nullptr;   // [kFields][nslots]
+  size_t nslots = 0;
+  double* d_lights = nullptr;   // [RT_MAX_LIGHTS][6]
+  int cached_lights = -1;       // light count currently in d_lights
+  double cached_light_data[RT_MAX_LIGHTS * 6] = {};
+  double delta = 0.0;
+  double root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};
+  long long bytes = 0;
+  int n_cu = 0;
+  int blocks_per_cu[kNumVariants] = {0, 0};
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool timed = false;
+};
+
+namespace {
+
+template <typename T>
+int upload(T** dst, const std::vector<T>& src, long long& bytes) {
+  const size_t n = std::max<size_t>(src.size(), 1);
+  HIP_TRY(hipMalloc(reinterpret_cast<void**>(dst), n * sizeof(T)));
+  if (!src.empty()) HIP_TRY(hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
+  bytes += (long long)(n * sizeof(T));
+  return RT_OK;
+}
+
+int validate(const rt_scene_soa* s, const rt_bvh_soa* b) {
+  if (!s || !b) return fail(RT_ERR_INVALID, "rt_scene_upload: null scene or bvh");
+  if (s->n_vertex_idx % 3 != 0 || s->n_vertex_idx < 0 || s->n_vertices < 0 || s->n_meshes < 0)
+    return fail(RT_ERR_INVALID, "rt_scene_upload: inconsistent counts");
+  const long long nt = s->n_vertex_idx / 3;
+  if (nt > 0 && (b->n_nodes < 1 || b->n_nodes > 2 * nt - 1))
+    return fail(RT_ERR_INVALID, "rt_scene_upload: bvh node count out of range");
+  for (long long i = 0; i < s->n_vertex_idx; ++i)
+    if (s->vertex_idx[i] < 0 || s->vertex_idx[i] >= s->n_vertices)
+      return fail(RT_ERR_INVALID, "rt_scene_upload: vertex index out of range");
+  for (int m = 0; m < s->n_meshes; ++m) {
+    if (s->mesh_draw_mode[m] != RT_DRAW_FLAT && s->mesh_draw_mode[m] != RT_DRAW_PHONG)
+      return fail(RT_ERR_INVALID, "rt_scene_upload: invalid draw mode (mytracer_gpu.cu:507)");
+    if (s->mesh_tex_width[m] > 0) {
+      if (s->mesh_tex_height[m] <= 0 || s->mesh_tex_offset[m] < 0 ||
+          s->mesh_tex_offset[m] + (long long)s->mesh_tex_width[m] * s->mesh_tex_height[m] > s->n_texels)
+        return fail(RT_ERR_INVALID, "rt_scene_upload: texture range out of bounds");
+    }
+  }
+  for (int v = 0; v < s->n_vertices; ++v)
+    if (s->vertex_mesh_id[v] < 0 || s->vertex_mesh_id[v] >= s->n_meshes)
+      return fail(RT_ERR_INVALID, "rt_scene_upload: vertex mesh id out of range");
+  for (int n = 0; n < b->n_nodes; ++n) {
+    if (b->tri_count[n] < 0 || b->first_tri[n] < 0 || (long long)b->first_tri[n] + b->tri_count[n] > nt)
+      return fail(RT_ERR_INVALID, "rt_scene_upload: bvh leaf range out of bounds");
+    if (b->tri_count[n] == 0 && (b->left_child[n] < 1 || b->left_child[n] + 1 >= b->n_nodes))
+      return fail(RT_ERR_INVALID, "rt_scene_upload: bvh child index out of range");
+  }
+  return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* rt_last_error(void) { return g_error.c_str(); }
+
+const char* rt_build_info(void) {
+  return "librt_hip: gfx950 persistent flattened render kernel; variants stats{0,1}; "
+         "fp32 2-wide nodes, fp64 triangles/shading, dynamic LDS stack, global path state, 8 XCD work heads";
+}
+
+int rt_scene_upload(const rt_scene_soa* s, const rt_bvh_soa* b, int device, rt_scene** out) {
+  if (!out) return fail(RT_ERR_INVALID, "rt_scene_upload: null out");
+  *out = nullptr;
+  int rc = validate(s, b);
+  if (rc != RT_OK) return rc;
+  const long long nt = s->n_vertex_idx / 3;
+
+  // ---- delta: conservative growth of the fp32 boxes ----
+  double M = 0.0;
+  for (long long k = 0; k < 3LL * s->n_vertices; ++k) M = std::max(M, std::fabs(s->vertex_pos[k]));
+  if (!(M > 0.0)) M = 1.0;
+  const double delta = M * 9.5367431640625e-07;   // 2^-20
+
+  // ---- 2-wide fp32 nodes in preorder ----
+  std::vector<GNode> nodes;
+  std::vector<uint32_t> last(std::max<long long>(nt, 1), 0);
+  int depth = 0;
+  auto set_child = [&](GNode& g, int s_, int c) {
+    float* ax[3] = {g.x, g.y, g.z};
+    for (int k = 0; k < 3; ++k) {
+      ax[k][2 * s_] = round_down_host(b->bb_min[3 * (size_t)c + k] - delta);
+      ax[k][2 * s_ + 1] = round_up_host(b->bb_max[3 * (size_t)c + k] + delta);
+    }
+  };
+  if (nt > 0) {
+    for (int n = 0; n < b->n_nodes; ++n)
+      if (b->tri_count[n] > 0) last[b->first_tri[n] + b->tri_count[n] - 1] = 1;
+    if (b->tri_count[0] > 0) {   // root is a leaf
+      GNode g{};
+      set_child(g, 0, 0);
+      g.ref[0] = kLeaf | (uint32_t)b->first_tri[0];
+      g.ref[1] = kEmpty;
+      nodes.push_back(g);
+      depth = 1;
+    } else {
+      std::vector<int> gidx(b->n_nodes, -1);
+      std::vector<std::pair<int, int>> stk;   // (node, depth)
+      std::vector<int> order;
+      stk.emplace_back(0, 0);
+      while (!stk.empty()) {
+        const auto [n, d] = stk.back();
+        stk.pop_back();
+        gidx[n] = (int)order.size();
+        order.push_back(n);
+        depth = std::max(depth, d + 1);
+        const int l = b->left_child[n], r = l + 1;
+        if (b->tri_count[r] == 0) stk.emplace_back(r, d + 1);
+        if (b->tri_count[l] == 0) stk.emplace_back(l, d + 1);
+      }
+      nodes.resize(order.size());
+      for (size_t gi = 0; gi < order.size(); ++gi) {
+        const int n = order[gi];
+        GNode& g = nodes[gi];
+        std::memset(&g, 0, sizeof g);
+        for (int s_ = 0; s_ < 2; ++s_) {
+          const int c = b->left_child[n] + s_;
+          set_child(g, s_, c);
+          g.ref[s_] = (b->tri_count[c] == 0) ? (uint32_t)gidx[c] : (kLeaf | (uint32_t)b->first_tri[c]);
+        }
+      }
+    }
+  }
+  if (depth > kMaxDepth)
+    return fail(RT_ERR_UNSUPPORTED, "rt_scene_upload: BVH deeper than 128 levels (LDS stack budget)");
+
+  // ---- triangle records / shading data in leaf order ----
+  std::vector<GTri> tris((size_t)nt);
+  std::vector<TriShade> shade((size_t)nt);
+  for (long long i = 0; i < nt; ++i) {
+    const int v0 = s->vertex_idx[3 * i], v1 = s->vertex_idx[3 * i + 1], v2 = s->vertex_idx[3 * i + 2];
+    const double* p0 = s->vertex_pos + 3 * (size_t)v0;
+    const double* p1 = s->vertex_pos + 3 * (size_t)v1;
+    const double* p2 = s->vertex_pos + 3 * (size_t)v2;
+    GTri& T = tris[i];
+    for (int k = 0; k < 3; ++k) {
+      T.e1[k] = p0[k] - p2[k];
+      T.e2[k] = p1[k] - p2[k];
+      T.p2[k] = p2[k];
+    }
+    T.mesh = s->vertex_mesh_id[v0];                 // meshId = vertexMeshId_[vi0], mytracer_gpu.cu:492
+    T.last = last[i];
+    TriShade& sh = shade[i];
+    sh.v[0] = v0; sh.v[1] = v1; sh.v[2] = v2;
+    for (int k = 0; k < 3; ++k) sh.t[k] = s->texture_idx ? s->texture_idx[3 * i + k] : -1;
+    sh.pad[0] = sh.pad[1] = 0;
+    if (s->mesh_tex_width[T.mesh] > 0)
+      for (int k = 0; k < 3; ++k)
+        if (sh.t[k] < 0 || sh.t[k] >= s->n_tex_coords)
+          return fail(RT_ERR_INVALID, "rt_scene_upload: textured mesh with invalid uv index");
+  }
+  std::vector<GMat> mats((size_t)s->n_meshes);
+  for (int m = 0; m < s->n_meshes; ++m) {
+    GMat& G = mats[m];
+    std::memset(&G, 0, sizeof G);
+    for (int k = 0; k < 3; ++k) {
+      G.ka[k] = s->mat_ambient[3 * m + k];
+      G.kd[k] = s->mat_diffuse[3 * m + k];
+      G.ks[k] = s->mat_specular[3 * m + k];
+    }
+    G.shininess = s->mat_shininess[m];
+    G.mirror = s->mat_mirror[m];
+    G.shadowable = s->mat_shadowable[m];
+    G.draw_mode = s->mesh_draw_mode[m];
+    G.tex_w = s->mesh_tex_width[m] > 0 ? s->mesh_tex_width[m] : -1;
+    G.tex_h = s->mesh_tex_height[m];
+    G.tex_off = s->mesh_tex_offset[m];
+  }
+  std::vector<double> fnorm(s->face_normals, s->face_normals + 3 * nt);
+  std::vector<double> vnorm(s->vertex_normals, s->vertex_normals + 3 * (size_t)s->n_vertices);
+  std::vector<double> tu(s->tex_u, s->tex_u + s->n_tex_coords), tv(s->tex_v, s->tex_v + s->n_tex_coords);
+  std::vector<unsigned char> texels(s->texels, s->texels + 3 * s->n_texels);
+
+  HIP_TRY(hipSetDevice(device));
+  auto* sc = new rt_scene();
+  sc->device = device;
+  long long bytes = 0;
+  rc = RT_OK;
+  if (rc == RT_OK) rc = upload(&sc->d_nodes, nodes, bytes);
+  if (rc == RT_OK) rc = upload(&sc->d_tris, tris, bytes);
+  if (rc == RT_OK) rc = upload(&sc->d_shade, shade, bytes);
+  if (rc == RT_OK) rc = upload(&sc->d_fnorm, fnorm, bytes);
+  if (rc == RT_OK) rc = upload(&sc->d_vnorm, vnorm, bytes);
+  if (rc == RT_OK) rc = upload(&sc->d_tu, tu, bytes);
+  if (rc == RT_OK) rc = upload(&sc->d_tv, tv, bytes);
+  if (rc == RT_OK) rc = upload(&sc->d_texels, texels, bytes);
+  if (rc == RT_OK) rc = upload(&sc->d_mats, mats, bytes);
+  if (rc == RT_OK) {
+    std::vector<unsigned long long> z(kCtrWords, 0);
+    rc = upload(&sc->d_ctr, z, bytes);
+  }
+  if (rc != RT_OK) {
+    rt_scene_free(sc);
+    return rc;
+  }
+  sc->n_gnodes = (int)nodes.size();
+  sc->n_tris = nt;
+  sc->n_meshes = s->n_meshes;
+  sc->depth = depth;
+  sc->stack_words = std::max(1, depth);
+  sc->delta = delta;
+  if (nt > 0)
+    for (int k = 0; k < 3; ++k) {
+      sc->root_lo[k] = b->bb_min[k] - delta;
+      sc->root_hi[k] = b->bb_max[k] + delta;
+    }
+  sc->bytes = bytes;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) { rt_scene_free(sc); return fail(RT_ERR_HIP, "hipGetDeviceProperties failed"); }
+  sc->n_cu = prop.multiProcessorCount;
+  const size_t lds = lds_bytes(sc->stack_words);
+  int max_blocks = 1;
+  for (int v = 0; v < kNumVariants; ++v) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(kVariants[v].fn), kBlock, lds) !=
+            hipSuccess || nb < 1)
+      nb = 1;
+    sc->blocks_per_cu[v] = nb;
+    max_blocks = std::max(max_blocks, nb);
+  }
+  sc->nslots = (size_t)sc->n_cu * max_blocks * kBlock;
+  if (hipMalloc(reinterpret_cast<void**>(&sc->d_pstate), sc->nslots * kFields * sizeof(double)) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void**>(&sc->d_lights), RT_MAX_LIGHTS * 6 * sizeof(double)) != hipSuccess) {
+    rt_scene_free(sc);
+    return fail(RT_ERR_HIP, "hipMalloc of path state failed");
+  }
+  sc->bytes += (long long)(sc->nslots * kFields * sizeof(double) + RT_MAX_LIGHTS * 6 * sizeof(double));
+  if (hipEventCreate(&sc->ev0) != hipSuccess || hipEventCreate(&sc->ev1) != hipSuccess) {
+    rt_scene_free(sc);
+    return fail(RT_ERR_HIP, "hipEventCreate failed");
+  }
+  *out = sc;
+  return RT_OK;
+}
+
+long long rt_scene_device_bytes(const rt_scene* s) { return s ? s->bytes : 0; }
+
+int rt_rows_in_shard(const rt_render_params* p) {
+  if (!p) return 0;
+  const int H = p->camera.height;
+  const int sc = p->stripe_count > 0 ? p->stripe_count : 1;
+  const int sh = p->stripe_height > 0 ? p->stripe_height : 1;
+  if (sc == 1) {
+    const int rb = std::max(0, p->row_begin);
+    const int re = (p->row_end <= 0 || p->row_end > H) ? H : p->row_end;
+    return std::max(0, re - rb);
+  }
+  int rows = 0;
+  for (int y = 0; y < H; ++y)
+    if ((y / sh) % sc == p->stripe_index) rows++;
+  return rows;
+}
+
+int rt_launch_compute_image(rt_scene* sc, const rt_render_params* p, void* d_out, rt_stats* stats, void* stream) {
+  if (!sc || !p || !d_out) return fail(RT_ERR_INVALID, "rt_launch_compute_image: null argument");
+  if (p->camera.width <= 0 || p->camera.height <= 0) return fail(RT_ERR_INVALID, "bad image size");
+  if (p->n_lights < 0 || p->n_lights > RT_MAX_LIGHTS) return fail(RT_ERR_INVALID, "n_lights out of range");
+  if (p->spp_n < 1 || p->spp_n > 64) return fail(RT_ERR_INVALID, "spp_n must be in [1, 64]");
+  if (p->max_depth < 0) return fail(RT_ERR_INVALID, "max_depth must be >= 0");
+  if (p->out_format != RT_OUT_RGB_F32 && p->out_format != RT_OUT_RGB_F64) return fail(RT_ERR_INVALID, "bad out_format");
+  const int scount = p->stripe_count > 0 ? p->stripe_count : 1;
+  if (p->stripe_index < 0 || p->stripe_index >= scount) return fail(RT_ERR_INVALID, "stripe_index out of range");
+  if (scount > 1 && (p->row_begin != 0 || (p->row_end > 0 && p->row_end != p->camera.height)))
+    return fail(RT_ERR_INVALID, "row ranges cannot be combined with stripe_count > 1");
+  const int rows = rt_rows_in_shard(p);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  HIP_TRY(hipSetDevice(sc->device));
+
+  KParams P;
+  std::memset(&P, 0, sizeof P);
+  P.nodes = sc->d_nodes; P.tris = sc->d_tris; P.shade = sc->d_shade; P.fnorm = sc->d_fnorm;
+  P.vnorm = sc->d_vnorm; P.tu = sc->d_tu; P.tv = sc->d_tv; P.texels = sc->d_texels; P.mats = sc->d_mats;
+  P.ctr = sc->d_ctr;
+  P.out = d_out;
+  P.n_gnodes = sc->n_gnodes;
+  P.out_fmt = p->out_format;
+  for (int k = 0; k < 3; ++k) {
+    P.root_lo[k] = sc->root_lo[k]; P.root_hi[k] = sc->root_hi[k];
+    P.eye[k] = p->camera.eye[k]; P.ll[k] = p->camera.lower_left[k];
+    P.xd[k] = p->camera.x_dir[k]; P.yd[k] = p->camera.y_dir[k];
+    P.bg[k] = p->background[k]; P.amb[k] = p->ambience[k];
+  }
+  P.W = p->camera.width;
+  P.H = p->camera.height;
+  P.n_lights = p->n_lights;
+  P.max_depth = p->max_depth;
+  {  // lights live in device memory; re-uploaded (device-synchronising) only when they change
+    double ld[RT_MAX_LIGHTS * 6] = {};
+    for (int i = 0; i < p->n_lights; ++i)
+      for (int k = 0; k < 3; ++k) { ld[6 * i + k] = p->lights[i].position[k]; ld[6 * i + 3 + k] = p->lights[i].color[k]; }
+    if (sc->cached_lights != p->n_lights || std::memcmp(ld, sc->cached_light_data, sizeof(double) * 6 * p->n_lights) != 0) {
+      HIP_TRY(hipDeviceSynchronize());
+      HIP_TRY(hipMemcpy(sc->d_lights, ld, sizeof ld, hipMemcpyHostToDevice));
+      std::memcpy(sc->cached_light_data, ld, sizeof ld);
+      sc->cached_lights = p->n_lights;
+    }
+  }
+  P.lights = sc->d_lights;
+  P.pstate = sc->d_pstate;
+  P.nslots = sc->nslots;
+  P.spp_n = p->spp_n;
+  P.row_begin = scount == 1 ? std::max(0, p->row_begin) : 0;
+  P.stripe_h = p->stripe_height > 0 ? p->stripe_height : 1;
+  P.stripe_count = scount;
+  P.stripe_index = p->stripe_index;
+  P.rows = rows;
+  P.tiles_x = (P.W + 7) / 8;
+  P.n_tiles = (long long)P.tiles_x * ((rows + 7) / 8);
+
+  const bool want_stats = (p->flags & RT_FLAG_TRAVERSAL_STATS) != 0;
+  const int v = want_stats ? 1 : 0;
+  const size_t lds = lds_bytes(sc->stack_words);
+  const long long waves_needed = (P.n_tiles * 64 + 63) / 64;
+  long long blocks = (long long)sc->n_cu * sc->blocks_per_cu[v];
+  blocks = std::max<long long>(1, std::min<long long>(blocks, (waves_needed + 3) / 4));
+  blocks = std::min<long long>(blocks, (long long)(sc->nslots / kBlock));
+
+  HIP_TRY(hipMemsetAsync(sc->d_ctr, 0, kCtrWords * sizeof(unsigned long long), st));
+  HIP_TRY(hipEventRecord(sc->ev0, st));
+  if (rows > 0) {
+    void* args[] = {&P};
+    HIP_TRY(hipLaunchKernel(reinterpret_cast<const void*>(kVariants[v].fn), dim3((unsigned)blocks), dim3(kBlock),
+                            args, lds, st));
+  }
+  HIP_TRY(hipEventRecord(sc->ev1, st));
+  sc->timed = true;
+  if (stats) {
+    HIP_TRY(hipStreamSynchronize(st));
+    unsigned long long c[kCtrWords];
+    HIP_TRY(hipMemcpy(c, sc->d_ctr, sizeof c, hipMemcpyDeviceToHost));
+    std::memset(stats, 0, sizeof *stats);
+    stats->primary_rays = (long long)c[CS_PRIMARY];
+    stats->shadow_rays = (long long)c[CS_SHADOW];
+    stats->reflection_rays = (long long)c[CS_REFLECT];
+    stats->node_visits = (long long)c[CS_NODES];
+    stats->tri_tests = (long long)c[CS_TRIS];
+    stats->closest_hits = (long long)c[CS_HITS];
+    stats->pixels = (long long)c[CS_PIXELS];
+  }
+  return RT_OK;
+}
+
+int rt_render_to_host(rt_scene* sc, const rt_render_params* p, void* host_out, rt_stats* stats) {
+  if (!sc || !p || !host_out) return fail(RT_ERR_INVALID, "rt_render_to_host: null argument");
+  HIP_TRY(hipSetDevice(sc->device));
+  const int rows = rt_rows_in_shard(p);
+  const size_t elem = p->out_format == RT_OUT_RGB_F64 ? sizeof(double) : sizeof(float);
+  const size_t bytes = std::max<size_t>(1, (size_t)rows * p->camera.width * 3 * elem);
+  void* d = nullptr;
+  HIP_TRY(hipMalloc(&d, bytes));
+  rt_stats local;
+  int rc = rt_launch_compute_image(sc, p, d, stats ? stats : &local, nullptr);
+  if (rc == RT_OK) {
+    const hipError_t e = hipMemcpy(host_out, d, (size_t)rows * p->camera.width * 3 * elem, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) rc = fail(RT_ERR_HIP, std::string("hipMemcpy D2H: ") + hipGetErrorString(e));
+  }
+  (void)hipFree(d);
+  return rc;
+}
+
+int rt_last_kernel_ms(rt_scene* sc, float* ms) {
+  if (!sc || !ms || !sc->timed) return fail(RT_ERR_INVALID, "rt_last_kernel_ms: no launch recorded");
+  HIP_TRY(hipEventSynchronize(sc->ev1));
+  HIP_TRY(hipEventElapsedTime(ms, sc->ev0, sc->ev1));
+  return RT_OK;
+}
+
+void rt_scene_free(rt_scene* sc) {
+  if (!sc) return;
+  (void)hipSetDevice(sc->device);
+  void* ptrs[] = {sc->d_nodes, sc->d_tris, sc->d_shade, sc->d_fnorm, sc->d_vnorm, sc->d_tu,
+                  sc->d_tv, sc->d_texels, sc->d_mats, sc->d_ctr, sc->d_pstate, sc->d_lights};
+  for (void* q : ptrs)
+    if (q) (void)hipFree(q);
+  if (sc->ev0) (void)hipEventDestroy(sc->ev0);
+  if (sc->ev1) (void)hipEventDestroy(sc->ev1);
+  delete sc;
+}
+
+}  // extern "C"

@@ -1,0 +1,108 @@
+// cli.cpp — rt_render: command-line front end of the MI355X render path.
+//
+// Host-side mirror of the reference's Raytracer flow (mytracer.cpp:54-60 and
+// 123-159): init (read/generate scene, compute normals, build_Data, BVH
+// initSoA) then compute_image on the GPU and write the image.  Everything goes
+// through the two C-ABIs (rt_host.h, rt_hip.h); no HIP headers here.
+//
+//   rt_render --scene office|cornell|random_tris|spheres|path.sce
+//             [--width W --height H --spp N --max-depth D --tris N --seed S
+//              --detail K --device I --frames F --out image.ppm]
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../../include/rt_hip.h"
+#include "../../../include/rt_host.h"
+
+namespace {
+
+class Raytracer {
+ public:
+  ~Raytracer() {
+    rt_scene_free(gpu_);
+    rt_host_free(host_);
+  }
+  // Raytracer::init_cuda equivalent.
+  bool init(const std::string& scene, const rt_gen_params& gp, int device) {
+    int rc = (scene.size() > 4 && scene.substr(scene.size() - 4) == ".sce") ? rt_host_load(scene.c_str(), &host_)
+                                                                              : rt_host_generate(scene.c_str(), &gp, &host_);
+    if (rc != RT_OK) return error(rt_host_last_error());
+    double build_s = 0;
+    if (rt_host_prepare(host_, &build_s) != RT_OK) return error(rt_host_last_error());
+    std::printf("scene %s: %lld triangles, BVH depth %d, host build %.3f s\n", scene.c_str(),
+                rt_host_triangle_count(host_), rt_host_bvh_depth(host_), build_s);
+    if (rt_scene_upload(rt_host_soa(host_), rt_host_bvh(host_), device, &gpu_) != RT_OK) return error(rt_last_error());
+    std::printf("uploaded %.1f MB to device %d\n", rt_scene_device_bytes(gpu_) / 1e6, device);
+    return true;
+  }
+  // Raytracer::compute_image_cuda equivalent.
+  bool compute_image(int width, int height, int spp, int max_depth, int frames) {
+    if (rt_host_render_params(host_, width, height, spp, &params_) != RT_OK) return error(rt_host_last_error());
+    if (max_depth >= 0) params_.max_depth = max_depth;
+    image_.assign(3 * (size_t)params_.camera.width * params_.camera.height, 0.f);
+    for (int f = 0; f < frames; ++f) {
+      rt_stats st;
+      if (rt_render_to_host(gpu_, &params_, image_.data(), &st) != RT_OK) return error(rt_last_error());
+      float ms = 0;
+      rt_last_kernel_ms(gpu_, &ms);
+      const long long rays = st.primary_rays + st.shadow_rays + st.reflection_rays;
+      std::printf("frame %d: %dx%d spp %d  kernel %.3f ms  rays %lld (P %lld S %lld R %lld)  %.1f Mrays/s\n", f,
+                  params_.camera.width, params_.camera.height, params_.spp_n * params_.spp_n, ms, rays,
+                  st.primary_rays, st.shadow_rays, st.reflection_rays, rays / (ms * 1e3));
+    }
+    return true;
+  }
+  bool write(const std::string& path) {
+    if (rt_write_ppm(path.c_str(), image_.data(), params_.camera.width, params_.camera.height) != RT_OK)
+      return error(rt_host_last_error());
+    std::printf("wrote %s\n", path.c_str());
+    return true;
+  }
+
+ private:
+  bool error(const char* msg) {
+    std::fprintf(stderr, "rt_render: %s\n", msg);
+    return false;
+  }
+  rt_host_scene* host_ = nullptr;
+  rt_scene* gpu_ = nullptr;
+  rt_render_params params_{};
+  std::vector<float> image_;
+};
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  std::string scene = "office", out;
+  int width = 0, height = 0, spp = 1, max_depth = -1, device = 0, frames = 1;
+  rt_gen_params gp{};
+  gp.max_depth = -1;
+  for (int i = 1; i < argc; ++i) {
+    const std::string a = argv[i];
+    auto next = [&]() -> const char* {
+      if (i + 1 >= argc) { std::fprintf(stderr, "missing value for %s\n", a.c_str()); std::exit(2); }
+      return argv[++i];
+    };
+    if (a == "--scene") scene = next();
+    else if (a == "--width") width = std::atoi(next());
+    else if (a == "--height") height = std::atoi(next());
+    else if (a == "--spp") spp = std::atoi(next());
+    else if (a == "--max-depth") max_depth = std::atoi(next());
+    else if (a == "--tris") gp.n_triangles = std::atoll(next());
+    else if (a == "--seed") gp.seed = std::strtoull(next(), nullptr, 10);
+    else if (a == "--detail") gp.detail = std::atoi(next());
+    else if (a == "--device") device = std::atoi(next());
+    else if (a == "--frames") frames = std::atoi(next());
+    else if (a == "--out") out = next();
+    else { std::fprintf(stderr, "unknown option %s\n", a.c_str()); return 2; }
+  }
+  Raytracer rt;
+  if (!rt.init(scene, gp, device)) return 1;
+  if (!rt.compute_image(width, height, spp, max_depth, frames)) return 1;
+  if (!out.empty() && !rt.write(out)) return 1;
+  return 0;
+}

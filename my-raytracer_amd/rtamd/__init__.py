@@ -1,0 +1,254 @@
+"""rtamd — Python host mirror of the MI355X render path.
+
+Thin ctypes layer over the two C-ABIs built in-tree:
+  lib/librt_host.so  (include/rt_host.h)  scene load / generate, normals,
+                     SoA flattening, median-split BVH  (C++)
+  lib/librt_hip.so   (include/rt_hip.h)   device upload + the flattened HIP
+                     render kernel for gfx950
+The classes mirror the reference's host flow (Raytracer::init_cuda,
+mytracer.cpp:54-60; Raytracer::compute_image_cuda, mytracer.cpp:123-159).
+There is no CPU fallback: if a library is missing every call fails loudly.
+"""
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+from . import abi
+from .abi import RT_OK, RT_OUT_RGB_F32, RT_OUT_RGB_F64, RT_FLAG_TRAVERSAL_STATS  # noqa: F401
+
+PKG_ROOT = Path(__file__).resolve().parent.parent
+LIB_DIR = PKG_ROOT / "lib"
+HOST_LIB = LIB_DIR / "librt_host.so"
+HIP_LIB = LIB_DIR / "librt_hip.so"
+
+_host = None
+_hip = None
+
+
+class RtError(RuntimeError):
+    pass
+
+
+def host_lib():
+    global _host
+    if _host is None:
+        if not HOST_LIB.exists():
+            raise RtError(f"{HOST_LIB} not built: run `make -C my-raytracer_amd` or __graft_entry__.build()")
+        _host = abi.bind(C.CDLL(str(HOST_LIB)), abi.HOST_SYMBOLS)
+    return _host
+
+
+def hip_lib():
+    global _hip
+    if _hip is None:
+        if not HIP_LIB.exists():
+            raise RtError(f"{HIP_LIB} not built: run `make -C my-raytracer_amd` or __graft_entry__.build()")
+        _hip = abi.bind(C.CDLL(str(HIP_LIB)), abi.HIP_SYMBOLS)
+    return _hip
+
+
+def _check_host(rc, what):
+    if rc != RT_OK:
+        raise RtError(f"{what}: {host_lib().rt_host_last_error().decode()}")
+
+
+def _check_hip(rc, what):
+    if rc != RT_OK:
+        raise RtError(f"{what}: {hip_lib().rt_last_error().decode()}")
+
+
+def _np(ptr, count, dtype):
+    if count == 0:
+        return np.zeros(0, dtype=dtype)
+    return np.ctypeslib.as_array(ptr, shape=(count,)).view(dtype)
+
+
+class HostScene:
+    """Host-resident scene (rt_host_scene*)."""
+
+    def __init__(self, handle):
+        self._h = handle
+
+    @classmethod
+    def generate(cls, kind, width=0, height=0, n_triangles=0, seed=0, max_depth=-1, detail=0):
+        gp = abi.GenParams(width=width, height=height, n_triangles=n_triangles, seed=seed,
+                           max_depth=max_depth, detail=detail)
+        h = C.c_void_p()
+        _check_host(host_lib().rt_host_generate(kind.encode(), C.byref(gp), C.byref(h)), f"generate {kind}")
+        return cls(h)
+
+    @classmethod
+    def load(cls, path):
+        h = C.c_void_p()
+        _check_host(host_lib().rt_host_load(str(path).encode(), C.byref(h)), f"load {path}")
+        return cls(h)
+
+    @property
+    def handle(self):
+        if self._h is None:
+            raise RtError("scene closed")
+        return self._h
+
+    def close(self):
+        if self._h is not None:
+            host_lib().rt_host_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def prepare(self):
+        secs = C.c_double(0.0)
+        _check_host(host_lib().rt_host_prepare(self.handle, C.byref(secs)), "prepare")
+        return secs.value
+
+    @property
+    def raw(self):
+        return host_lib().rt_host_raw(self.handle)
+
+    @property
+    def soa(self):
+        p = host_lib().rt_host_soa(self.handle)
+        if not p:
+            raise RtError("scene not prepared")
+        return p
+
+    @property
+    def bvh(self):
+        p = host_lib().rt_host_bvh(self.handle)
+        if not p:
+            raise RtError("scene not prepared")
+        return p
+
+    def soa_arrays(self):
+        s = self.soa.contents
+        nt = s.n_vertex_idx // 3
+        return {
+            "vertex_pos": _np(s.vertex_pos, 3 * s.n_vertices, np.float64).reshape(-1, 3),
+            "vertex_normals": _np(s.vertex_normals, 3 * s.n_vertices, np.float64).reshape(-1, 3),
+            "vertex_mesh_id": _np(s.vertex_mesh_id, s.n_vertices, np.int32),
+            "face_normals": _np(s.face_normals, 3 * nt, np.float64).reshape(-1, 3),
+            "vertex_idx": _np(s.vertex_idx, s.n_vertex_idx, np.int32).reshape(-1, 3),
+            "texture_idx": _np(s.texture_idx, s.n_vertex_idx, np.int32).reshape(-1, 3),
+        }
+
+    def bvh_arrays(self):
+        b = self.bvh.contents
+        n = b.n_nodes
+        return {
+            "bb_min": _np(b.bb_min, 3 * n, np.float64).reshape(-1, 3),
+            "bb_max": _np(b.bb_max, 3 * n, np.float64).reshape(-1, 3),
+            "left_child": _np(b.left_child, n, np.int32),
+            "first_tri": _np(b.first_tri, n, np.int32),
+            "tri_count": _np(b.tri_count, n, np.int32),
+        }
+
+    def camera(self, width=0, height=0):
+        cam = abi.Camera()
+        _check_host(host_lib().rt_host_camera(self.handle, width, height, C.byref(cam)), "camera")
+        return cam
+
+    def render_params(self, width=0, height=0, spp_n=1):
+        p = abi.RenderParams()
+        _check_host(host_lib().rt_host_render_params(self.handle, width, height, spp_n, C.byref(p)),
+                    "render_params")
+        return p
+
+    def save(self, path):
+        _check_host(host_lib().rt_host_save(self.handle, str(path).encode()), f"save {path}")
+
+    @property
+    def triangle_count(self):
+        return int(host_lib().rt_host_triangle_count(self.handle))
+
+    @property
+    def bvh_depth(self):
+        return int(host_lib().rt_host_bvh_depth(self.handle))
+
+
+class DeviceScene:
+    """Scene resident on one MI355X (rt_scene*), uploaded from a prepared HostScene."""
+
+    def __init__(self, host_scene, device=0):
+        self._h = C.c_void_p()
+        self.device = device
+        _check_hip(hip_lib().rt_scene_upload(host_scene.soa, host_scene.bvh, device, C.byref(self._h)),
+                   "rt_scene_upload")
+
+    def close(self):
+        if self._h:
+            hip_lib().rt_scene_free(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def device_bytes(self):
+        return int(hip_lib().rt_scene_device_bytes(self._h))
+
+    def launch(self, params, d_out, stats=False, stream=None):
+        """Asynchronous render into a device buffer (int pointer); returns Stats if stats=True."""
+        st = abi.Stats() if stats else None
+        _check_hip(hip_lib().rt_launch_compute_image(self._h, C.byref(params), C.c_void_p(d_out),
+                                                     C.byref(st) if st is not None else None,
+                                                     C.c_void_p(stream) if stream else None),
+                   "rt_launch_compute_image")
+        return st
+
+    def render(self, params):
+        """Synchronous render to host; returns (image[rows, W, 3], Stats)."""
+        rows = rows_in_shard(params)
+        dtype = np.float64 if params.out_format == RT_OUT_RGB_F64 else np.float32
+        img = np.zeros((rows, params.camera.width, 3), dtype=dtype)
+        st = abi.Stats()
+        _check_hip(hip_lib().rt_render_to_host(self._h, C.byref(params), img.ctypes.data_as(C.c_void_p),
+                                               C.byref(st)), "rt_render_to_host")
+        return img, st
+
+    def last_kernel_ms(self):
+        ms = C.c_float(0.0)
+        _check_hip(hip_lib().rt_last_kernel_ms(self._h, C.byref(ms)), "rt_last_kernel_ms")
+        return ms.value
+
+
+def rows_in_shard(params):
+    return int(hip_lib().rt_rows_in_shard(C.byref(params)))
+
+
+def shard_rows(height, stripe_height, stripe_count, stripe_index):
+    """Global row ids a shard renders, in output order (rt_render_params rules)."""
+    y = np.arange(height)
+    return y[(y // stripe_height) % stripe_count == stripe_index]
+
+
+def write_ppm(path, img):
+    img = np.ascontiguousarray(img, dtype=np.float32)
+    h, w, _ = img.shape
+    _check_host(host_lib().rt_write_ppm(str(path).encode(), img.ctypes.data_as(C.POINTER(C.c_float)), w, h),
+                "rt_write_ppm")
+
+
+class Raytracer:
+    """Mirror of the reference's Raytracer host flow on the MI355X path."""
+
+    def __init__(self, scene="office", device=0, **gen):
+        if str(scene).endswith(".sce") or os.path.sep in str(scene):
+            self.host = HostScene.load(scene)
+        else:
+            self.host = HostScene.generate(scene, **gen)
+        self.build_seconds = self.host.prepare()
+        self.gpu = DeviceScene(self.host, device)
+
+    def compute_image(self, width=0, height=0, spp_n=1, out_format=RT_OUT_RGB_F32):
+        p = self.host.render_params(width, height, spp_n)
+        p.out_format = out_format
+        return self.gpu.render(p)

@@ -1,0 +1,151 @@
+"""ctypes mirror of include/rt_scene.h, include/rt_hip.h and include/rt_host.h.
+
+These structs are the plain-C boundary of the MI355X render path; keep them in
+lock-step with the headers (tests/test_abi.py checks sizes and symbols).
+"""
+import ctypes as C
+
+c_double3 = C.c_double * 3
+
+RT_OK = 0
+RT_ERR_INVALID = -1
+RT_ERR_HIP = -2
+RT_ERR_UNSUPPORTED = -3
+RT_MAX_LIGHTS = 16
+RT_DRAW_FLAT = 0
+RT_DRAW_PHONG = 1
+RT_OUT_RGB_F32 = 0
+RT_OUT_RGB_F64 = 1
+RT_FLAG_TRAVERSAL_STATS = 1
+
+
+class Material(C.Structure):
+    _fields_ = [("ambient", c_double3), ("diffuse", c_double3), ("specular", c_double3),
+                ("shininess", C.c_double), ("mirror", C.c_double), ("shadowable", C.c_int),
+                ("pad_", C.c_int)]
+
+
+class Texture(C.Structure):
+    _fields_ = [("width", C.c_int), ("height", C.c_int), ("rgb", C.POINTER(C.c_ubyte))]
+
+
+class Mesh(C.Structure):
+    _fields_ = [("n_vertices", C.c_int), ("positions", C.POINTER(C.c_double)),
+                ("n_triangles", C.c_int), ("tri_vertex", C.POINTER(C.c_int)),
+                ("n_uv", C.c_int), ("u", C.POINTER(C.c_double)), ("v", C.POINTER(C.c_double)),
+                ("tri_uv", C.POINTER(C.c_int)), ("draw_mode", C.c_int), ("pad_", C.c_int),
+                ("material", Material), ("texture", Texture)]
+
+
+class Sphere(C.Structure):
+    _fields_ = [("center", c_double3), ("radius", C.c_double), ("material", Material)]
+
+
+class Plane(C.Structure):
+    _fields_ = [("center", c_double3), ("normal", c_double3), ("material", Material)]
+
+
+class Light(C.Structure):
+    _fields_ = [("position", c_double3), ("color", c_double3)]
+
+
+class CameraDef(C.Structure):
+    _fields_ = [("eye", c_double3), ("center", c_double3), ("up", c_double3),
+                ("fovy", C.c_double), ("width", C.c_int), ("height", C.c_int)]
+
+
+class Camera(C.Structure):
+    _fields_ = [("eye", c_double3), ("lower_left", c_double3), ("x_dir", c_double3),
+                ("y_dir", c_double3), ("width", C.c_int), ("height", C.c_int)]
+
+
+class RawScene(C.Structure):
+    _fields_ = [("camera", CameraDef), ("background", c_double3), ("ambience", c_double3),
+                ("max_depth", C.c_int), ("n_lights", C.c_int), ("lights", C.POINTER(Light)),
+                ("n_meshes", C.c_int), ("meshes", C.POINTER(Mesh)),
+                ("n_spheres", C.c_int), ("spheres", C.POINTER(Sphere)),
+                ("n_planes", C.c_int), ("planes", C.POINTER(Plane))]
+
+
+class SceneSoA(C.Structure):
+    _fields_ = [("n_meshes", C.c_int), ("n_vertices", C.c_int), ("n_vertex_idx", C.c_int),
+                ("n_tex_coords", C.c_int), ("n_texels", C.c_longlong),
+                ("vertex_mesh_id", C.POINTER(C.c_int)), ("vertex_pos", C.POINTER(C.c_double)),
+                ("vertex_normals", C.POINTER(C.c_double)), ("face_normals", C.POINTER(C.c_double)),
+                ("vertex_idx", C.POINTER(C.c_int)), ("texture_idx", C.POINTER(C.c_int)),
+                ("tex_u", C.POINTER(C.c_double)), ("tex_v", C.POINTER(C.c_double)),
+                ("texels", C.POINTER(C.c_ubyte)), ("mesh_tex_width", C.POINTER(C.c_int)),
+                ("mesh_tex_height", C.POINTER(C.c_int)), ("mesh_tex_offset", C.POINTER(C.c_longlong)),
+                ("mesh_draw_mode", C.POINTER(C.c_int)), ("mat_ambient", C.POINTER(C.c_double)),
+                ("mat_diffuse", C.POINTER(C.c_double)), ("mat_specular", C.POINTER(C.c_double)),
+                ("mat_shininess", C.POINTER(C.c_double)), ("mat_mirror", C.POINTER(C.c_double)),
+                ("mat_shadowable", C.POINTER(C.c_int))]
+
+
+class BvhSoA(C.Structure):
+    _fields_ = [("n_nodes", C.c_int), ("bb_min", C.POINTER(C.c_double)),
+                ("bb_max", C.POINTER(C.c_double)), ("left_child", C.POINTER(C.c_int)),
+                ("first_tri", C.POINTER(C.c_int)), ("tri_count", C.POINTER(C.c_int))]
+
+
+class RenderParams(C.Structure):
+    _fields_ = [("camera", Camera), ("n_lights", C.c_int), ("max_depth", C.c_int),
+                ("lights", Light * RT_MAX_LIGHTS), ("background", c_double3),
+                ("ambience", c_double3), ("spp_n", C.c_int), ("row_begin", C.c_int),
+                ("row_end", C.c_int), ("stripe_height", C.c_int), ("stripe_count", C.c_int),
+                ("stripe_index", C.c_int), ("out_format", C.c_int), ("flags", C.c_int)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("primary_rays", C.c_longlong), ("shadow_rays", C.c_longlong),
+                ("reflection_rays", C.c_longlong), ("node_visits", C.c_longlong),
+                ("tri_tests", C.c_longlong), ("closest_hits", C.c_longlong),
+                ("pixels", C.c_longlong), ("reserved_", C.c_longlong)]
+
+    def as_dict(self):
+        return {name: int(getattr(self, name)) for name, _ in self._fields_ if name != "reserved_"}
+
+
+class GenParams(C.Structure):
+    _fields_ = [("width", C.c_int), ("height", C.c_int), ("n_triangles", C.c_longlong),
+                ("seed", C.c_ulonglong), ("max_depth", C.c_int), ("detail", C.c_int)]
+
+
+# Symbols each library must export (declared in include/*.h).
+HIP_SYMBOLS = {
+    "rt_scene_upload": (C.c_int, [C.POINTER(SceneSoA), C.POINTER(BvhSoA), C.c_int, C.POINTER(C.c_void_p)]),
+    "rt_scene_device_bytes": (C.c_longlong, [C.c_void_p]),
+    "rt_rows_in_shard": (C.c_int, [C.POINTER(RenderParams)]),
+    "rt_launch_compute_image": (C.c_int, [C.c_void_p, C.POINTER(RenderParams), C.c_void_p,
+                                          C.POINTER(Stats), C.c_void_p]),
+    "rt_render_to_host": (C.c_int, [C.c_void_p, C.POINTER(RenderParams), C.c_void_p, C.POINTER(Stats)]),
+    "rt_last_kernel_ms": (C.c_int, [C.c_void_p, C.POINTER(C.c_float)]),
+    "rt_scene_free": (None, [C.c_void_p]),
+    "rt_last_error": (C.c_char_p, []),
+    "rt_build_info": (C.c_char_p, []),
+}
+
+HOST_SYMBOLS = {
+    "rt_host_load": (C.c_int, [C.c_char_p, C.POINTER(C.c_void_p)]),
+    "rt_host_generate": (C.c_int, [C.c_char_p, C.POINTER(GenParams), C.POINTER(C.c_void_p)]),
+    "rt_host_raw": (C.POINTER(RawScene), [C.c_void_p]),
+    "rt_host_prepare": (C.c_int, [C.c_void_p, C.POINTER(C.c_double)]),
+    "rt_host_soa": (C.POINTER(SceneSoA), [C.c_void_p]),
+    "rt_host_bvh": (C.POINTER(BvhSoA), [C.c_void_p]),
+    "rt_host_camera": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(Camera)]),
+    "rt_host_render_params": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(RenderParams)]),
+    "rt_host_save": (C.c_int, [C.c_void_p, C.c_char_p]),
+    "rt_write_ppm": (C.c_int, [C.c_char_p, C.POINTER(C.c_float), C.c_int, C.c_int]),
+    "rt_host_triangle_count": (C.c_longlong, [C.c_void_p]),
+    "rt_host_bvh_depth": (C.c_int, [C.c_void_p]),
+    "rt_host_free": (None, [C.c_void_p]),
+    "rt_host_last_error": (C.c_char_p, []),
+}
+
+
+def bind(lib, table):
+    for name, (res, args) in table.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
