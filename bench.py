@@ -1,0 +1,228 @@
+"""bench.py — Mrays/s of the MI355X render path on the Office workload.
+
+Metric (BASELINE.json): Mrays/sec (primary + shadow + reflection), Office
+1920x1080 1 spp, on 1/2/4/8 MI355X.  The Office scene files are not in the
+reference, so the workload is the fixed-seed office_proxy.
+
+One step = one full frame: every rank renders its interleaved 16-row stripes
+(stripe = rank mod N) with one launch of the flattened HIP kernel, then rank 0
+gathers the stripes over RCCL (torch.distributed "nccl") and re-interleaves
+them into the final image.  Total work per step is fixed => "strong" scaling.
+
+Rays per frame are the canonical counts returned by the kernel's
+counters in an untimed launch.  Roofline: algorithmic bytes per launch =
+64*node_visits + 48*tri_tests + 64*closest_hits, from the
+instrumented kernel variant (its counters are pinned to the CPU oracle's
+replica by tests/test_gpu_parity.py), divided by the kernel duration measured
+with HIP events on the launch stream over the timed steps.
+
+cpu_baseline: the CPU oracle (C restatement of the reference's CPU renderer:
+recursive unordered fp64 BVH traversal, closest-hit shadow rays, OpenMP) timed
+on a deterministic row sample of the same frame, rank 0 / N=1 only.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       (N>1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "my-raytracer_amd"))
+import rtamd  # noqa: E402
+from rtamd.shard import StripeGather, max_rows as shard_max_rows  # noqa: E402
+
+HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+STRIPE_H = 16
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--scene", default="office")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=1, help="n: n*n stratified samples per pixel")
+    ap.add_argument("--tris", type=int, default=0, help="random_tris triangle count")
+    ap.add_argument("--cpu-row-stride", type=int, default=1, help="cpu_baseline renders every k-th row")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--save", default="", help="rank 0: save the gathered image (.npy)")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.gpus != world and world > 1:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE {world}")
+    n = world
+    torch.cuda.set_device(local)
+    if n > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    # ---- host side: scene, normals, SoA, median-split BVH (untimed) ----
+    gen = {"n_triangles": a.tris} if a.scene == "random_tris" and a.tris else {}
+    host = rtamd.HostScene.generate(a.scene, **gen)
+    build_s = host.prepare()
+    gpu = rtamd.DeviceScene(host, device=local)
+    params = host.render_params(a.width, a.height, a.spp)
+    params.stripe_height = STRIPE_H
+    params.stripe_count = n
+    params.stripe_index = rank
+    W = a.width
+    buf = torch.zeros((shard_max_rows(a.height, STRIPE_H, n), W, 3), dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+
+    # ---- counters: canonical rays + algorithmic bytes (untimed launches) ----
+    st = gpu.launch(params, buf.data_ptr(), stats=True, stream=stream)
+    params.flags = rtamd.RT_FLAG_TRAVERSAL_STATS
+    tst = gpu.launch(params, buf.data_ptr(), stats=True, stream=stream)
+    params.flags = 0
+    rays_local = st.primary_rays + st.shadow_rays + st.reflection_rays
+    alg_bytes_local = 64 * tst.node_visits + 48 * tst.tri_tests + 64 * tst.closest_hits
+
+    gather = StripeGather(a.height, W, STRIPE_H, n, rank, device="cuda")
+    image = None
+
+    starts, ends = [], []
+
+    def step(timed):
+        nonlocal image
+        if timed:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        gpu.launch(params, buf.data_ptr(), stats=False, stream=stream)
+        if timed:
+            e1.record()
+            starts.append(e0)
+            ends.append(e1)
+        image = gather(buf)   # N>1: RCCL gather of the stripes to rank 0 + re-interleave
+
+    for _ in range(a.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if n > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step(True)
+    if n > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
+    kernel_ms_avg = float(np.mean(kernel_ms))
+
+    tot = torch.tensor([rays_local, alg_bytes_local], dtype=torch.float64, device="cuda")
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if n > 1:
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    rays_total = float(tot[0])
+    elapsed = float(tmax[0])
+
+    if rank == 0:
+        if a.save:
+            np.save(a.save, image.float().cpu().numpy())
+        ms_per_step = elapsed / a.steps * 1e3
+        mrays = rays_total * a.steps / elapsed / 1e6
+        achieved = alg_bytes_local / (kernel_ms_avg * 1e-3) / 1e9
+        out = {
+            "metric": "Mrays/sec (primary+shadow+reflect), Office 1920x1080 1spp",
+            "value": round(mrays, 2),
+            "unit": "Mrays/s",
+            "n_gpus": n,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: fixed-seed office_proxy stand-in (reference Office scene files are absent)",
+            "config": {
+                "workload": f"{a.scene}_proxy {a.width}x{a.height} spp={a.spp * a.spp} depth={params.max_depth} "
+                            f"lights={params.n_lights}",
+                "triangles": host.triangle_count,
+                "bvh": f"reference median split, depth {host.bvh_depth}",
+                "rays_per_frame": int(rays_total),
+                "rays_breakdown_rank0": {"primary": st.primary_rays, "shadow": st.shadow_rays,
+                                         "reflection": st.reflection_rays},
+                "parallelism": f"row-stripes x{n} (16-row interleave) + RCCL gather" if n > 1 else "single GPU",
+                "host_bvh_build_s": round(build_s, 4),
+                "device_scene_MB": round(gpu.device_bytes / 1e6, 1),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                "traffic": None,
+                "kernel_ms_avg": round(kernel_ms_avg, 4),
+                "alg_bytes_per_launch": int(alg_bytes_local),
+                "alg_bytes_def": "64*node_visits + 48*tri_tests + 64*closest_hits (rank-0 launch)",
+            },
+            "cpu_baseline": None,
+        }
+        if n == 1 and not a.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(host, params, a)
+        print(json.dumps(out), flush=True)
+    if n > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(host, params, a):
+    """CPU oracle (reference CPU renderer restated in C, OpenMP) on every k-th row."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import pyoracle
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads = max(1, min(threads, 16))
+    orc = pyoracle.Oracle(host.raw, host)
+    ys = np.arange(0, a.height, a.cpu_row_stride)
+    xs = np.arange(a.width)
+    xy = np.stack(np.meshgrid(xs, ys), -1).reshape(-1, 2)
+    p = host.render_params(a.width, a.height, a.spp)
+    t0 = time.perf_counter()
+    _, cnt = orc.render_pixels(p, xy, pyoracle.MODE_REFERENCE, threads)
+    dt = time.perf_counter() - t0
+    rays = cnt.primary_rays + cnt.shadow_rays + cnt.reflection_rays
+    cpu_model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {
+        "value": round(rays / dt / 1e6, 4),
+        "unit": "Mrays/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"every {a.cpu_row_stride}th row of the same frame: {len(xy)} pixels, {rays} rays, "
+                  f"{dt:.2f} s; reference-CPU-semantics oracle (recursive unordered fp64 BVH, "
+                  f"closest-hit shadows); extrapolated full-frame {dt * a.cpu_row_stride:.1f} s",
+        "cpu_model": cpu_model,
+        "nproc": os.cpu_count(),
+        "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+    }
+
+
+if __name__ == "__main__":
+    main()

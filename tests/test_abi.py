@@ -1,0 +1,81 @@
+"""The C-ABI libraries load on CPU and export every symbol include/*.h declares;
+the ctypes mirror (rtamd/abi.py) matches the C struct layouts."""
+import ctypes as C
+import re
+import subprocess
+from pathlib import Path
+
+import pytest
+
+import rtamd
+from rtamd import abi
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def declared(header):
+    text = (ROOT / "include" / header).read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(rt_[a-z0-9_]+)\s*\(", text)))
+
+
+def exported(lib):
+    out = subprocess.run(["nm", "-D", "--defined-only", str(lib)], capture_output=True, text=True, check=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if line.split()}
+
+
+@pytest.mark.parametrize("header,lib", [("rt_hip.h", rtamd.HIP_LIB), ("rt_host.h", rtamd.HOST_LIB)])
+def test_every_declared_symbol_exported(header, lib):
+    syms = declared(header)
+    assert syms, header
+    missing = [s for s in syms if s not in exported(lib)]
+    assert not missing, missing
+
+
+def test_ctypes_tables_cover_headers():
+    assert set(declared("rt_hip.h")) == set(abi.HIP_SYMBOLS)
+    assert set(declared("rt_host.h")) == set(abi.HOST_SYMBOLS)
+
+
+def test_libraries_load_and_report():
+    assert b"gfx950" in rtamd.hip_lib().rt_build_info()
+    assert rtamd.host_lib().rt_host_last_error() is not None
+
+
+def test_struct_layouts_match_c(tmp_path):
+    structs = {"rt_material": abi.Material, "rt_texture": abi.Texture, "rt_mesh": abi.Mesh,
+               "rt_sphere": abi.Sphere, "rt_plane": abi.Plane, "rt_light": abi.Light,
+               "rt_camera_def": abi.CameraDef, "rt_camera": abi.Camera, "rt_raw_scene": abi.RawScene,
+               "rt_scene_soa": abi.SceneSoA, "rt_bvh_soa": abi.BvhSoA, "rt_render_params": abi.RenderParams,
+               "rt_stats": abi.Stats, "rt_gen_params": abi.GenParams}
+    src = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{ROOT}/include/rt_host.h"', "int main(void){"]
+    for name in structs:
+        src.append(f'printf("{name} %zu\\n", sizeof({name}));')
+    src.append('printf("params.out_format %zu\\n", offsetof(rt_render_params, out_format));')
+    src.append('printf("soa.mat_shadowable %zu\\n", offsetof(rt_scene_soa, mat_shadowable));')
+    src.append("return 0;}")
+    (tmp_path / "sizes.c").write_text("\n".join(src))
+    subprocess.run(["gcc", "-o", str(tmp_path / "sizes"), str(tmp_path / "sizes.c")], check=True)
+    out = subprocess.run([str(tmp_path / "sizes")], capture_output=True, text=True, check=True).stdout
+    got = dict(line.split() for line in out.splitlines())
+    for name, cls in structs.items():
+        assert int(got[name]) == C.sizeof(cls), name
+    assert int(got["params.out_format"]) == abi.RenderParams.out_format.offset
+    assert int(got["soa.mat_shadowable"]) == abi.SceneSoA.mat_shadowable.offset
+
+
+def test_hip_entry_points_reject_bad_arguments():
+    lib = rtamd.hip_lib()
+    assert lib.rt_scene_upload(None, None, 0, C.byref(C.c_void_p())) == abi.RT_ERR_INVALID
+    assert b"null" in lib.rt_last_error()
+    assert lib.rt_launch_compute_image(None, None, None, None, None) == abi.RT_ERR_INVALID
+    p = abi.RenderParams()
+    p.camera.height = 100
+    p.stripe_height, p.stripe_count, p.stripe_index = 16, 3, 1
+    assert lib.rt_rows_in_shard(C.byref(p)) == len(rtamd.shard_rows(100, 16, 3, 1))
+
+
+def test_shard_rows_partition_the_image():
+    for h, sh, n in [(1080, 16, 8), (1080, 16, 3), (17, 4, 2), (5, 16, 8)]:
+        rows = sorted(sum((list(rtamd.shard_rows(h, sh, n, r)) for r in range(n)), []))
+        assert rows == list(range(h))
