@@ -91,7 +91,9 @@ enum {
 
 /* Flags of rt_render_params.flags. */
 enum {
-  RT_FLAG_TRAVERSAL_STATS = 1  /* instrumented kernel: counts node visits / triangle tests */
+  RT_FLAG_TRAVERSAL_STATS = 1, /* canonical counters: 2-wide traversal (the one the oracle replicates),
+                                  counts node visits / triangle tests / closest hits */
+  RT_FLAG_WIDE_STATS = 2       /* same counters on the production 4-wide traversal (diagnostics) */
 };
 
 /* One render call.  Rows are rendered as interleaved stripes:
@@ -160,6 +162,13 @@ int rt_render_to_host(rt_scene* scene, const rt_render_params* p, void* host_out
 /* Milliseconds of the last launch on this scene, measured with hipEvents
  * recorded around the kernel on its stream (valid after the stream syncs). */
 int rt_last_kernel_ms(rt_scene* scene, float* ms);
+
+/* Diagnostics: raw device counter words of the last launch (synchronises the
+ * device).  Words [8,16) = rt_stats order; with a STATS flag, words [16,26) =
+ * node-loop iterations / active lanes, leaf-loop iterations / active lanes,
+ * traverse / shade / refill cycles (s_memtime), outer iterations, traversal
+ * rounds / active lanes (per wave, summed).  Returns the number of words copied. */
+int rt_debug_counters(rt_scene* scene, unsigned long long* out, int n);
 
 void rt_scene_free(rt_scene* scene);
 

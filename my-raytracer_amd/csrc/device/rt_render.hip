@@ -47,13 +47,20 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kGroups = 8;          // work heads (XCD groups)
 constexpr int kRefill = 16;         // refill a wave when this many lanes are idle
-constexpr int kCtrWords = 16;       // [0,8) work heads, [8,16) stats
+constexpr int kCtrWords = 32;       // [0,8) work heads, [8,16) stats, [16,32) diagnostics
 
 enum : int { ST_FETCH = 0, ST_CLOSEST = 1, ST_SHADOW = 2, ST_DONE = 3 };
 enum : int { CS_PRIMARY = 8, CS_SHADOW, CS_REFLECT, CS_NODES, CS_TRIS, CS_HITS, CS_PIXELS };
+// diagnostics (STATS variants only): wave-level loop iterations and the active
+// lanes summed over them (SIMD efficiency), s_memtime cycles per phase.
+enum : int {
+  CD_NODE_ITERS = 16, CD_NODE_LANES, CD_LEAF_ITERS, CD_LEAF_LANES, CD_TRAV_CYCLES, CD_SHADE_CYCLES,
+  CD_FETCH_CYCLES, CD_OUTER_ITERS, CD_TRAV_ROUNDS, CD_TRAV_ROUND_LANES
+};
 
 struct KParams {
   const GNode* nodes;
+  const GNode4* nodes4;
   const GTri* tris;
   const TriShade* shade;
   const double* fnorm;
@@ -136,6 +143,12 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
   return v;
 }
 
+// Counts one wave-level iteration (and its active lanes) on the first active lane.
+__device__ __forceinline__ void wave_tick(unsigned long long& iters, unsigned long long& lanes, int lane) {
+  const unsigned long long m = __ballot(1);
+  if (lane == __ffsll((long long)m) - 1) { iters++; lanes += __popcll(m); }
+}
+
 struct TriOps {
   D3 e1, e2, p2;
   int mesh;
@@ -177,7 +190,14 @@ struct RaySlots {
 //             global path state and write their next ray (if any) to LDS.
 // Nothing but a few ids is live across the phase boundary, which keeps the
 // kernel at 4 waves/SIMD despite fp64 shading.
-template <bool STATS>
+__device__ __forceinline__ float f4c(const float4& v, int c) {
+  return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
+}
+__device__ __forceinline__ uint32_t u4c(const uint4& v, int c) {
+  return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
+}
+
+template <int WIDTH, bool STATS>
 __global__ void __launch_bounds__(kBlock, 4) render_kernel(KParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   double* lds_d = reinterpret_cast<double*>(lds_raw);
@@ -210,6 +230,10 @@ __global__ void __launch_bounds__(kBlock, 4) render_kernel(KParams P) {
   bool shadow_hit = false;
   unsigned c_primary = 0, c_shadow = 0, c_refl = 0, c_hits = 0;
   unsigned long long c_nodes = 0, c_tris = 0;
+  unsigned long long d_node_it = 0, d_node_ln = 0, d_leaf_it = 0, d_leaf_ln = 0;
+  unsigned long long d_trav = 0, d_shade = 0, d_fetch = 0, d_outer = 0, d_round_it = 0, d_round_ln = 0;
+  unsigned long long t_stamp = 0;
+  auto stamp = [&]() -> unsigned long long { return STATS ? __builtin_amdgcn_s_memtime() : 0ull; };
 
   // Ray(o, d): stores origin, normalised direction and t-limit to the LDS slot.
   auto emit_ray = [&](D3 o, D3 dir, double t_limit) {
@@ -238,6 +262,7 @@ __global__ void __launch_bounds__(kBlock, 4) render_kernel(KParams P) {
   };
 
   for (;;) {
+    if (STATS) { d_outer++; t_stamp = stamp(); }
     // ---------------- refill idle lanes (one atomic per wave) ----------------
     unsigned long long m_fetch = __ballot(state == ST_FETCH);
     unsigned long long m_busy = __ballot(state == ST_CLOSEST || state == ST_SHADOW);
@@ -285,6 +310,7 @@ __global__ void __launch_bounds__(kBlock, 4) render_kernel(KParams P) {
       continue;
     }
 
+    if (STATS) { const unsigned long long t = stamp(); d_fetch += t - t_stamp; t_stamp = t; }
     // ================= TRAVERSE phase =================
     {
       const bool anyhit = (state == ST_SHADOW);
@@ -336,14 +362,22 @@ __global__ void __launch_bounds__(kBlock, 4) render_kernel(KParams P) {
       const float ofy = (float)(ro.y + t_off * rd.y);
       const float ofz = (float)(ro.z + t_off * rd.z);
       const float ivx = inv[0], ivy = inv[1], ivz = inv[2];
+      // 4-wide node: per-ray near/far plane byte offsets (lo at +0, hi at +16 of each axis
+      // block) and o*inv, so a slab is one FMA: t = plane*inv - o*inv.  Conservative under
+      // the delta box growth; only the 2-wide canonical kernel replicates the
+      // oracle's sub-then-mul bit for bit.
+      const uint32_t nxo = ivx >= 0.f ? 0u : 16u, nyo = ivy >= 0.f ? 32u : 48u, nzo = ivz >= 0.f ? 64u : 80u;
+      const float oix = ofx * ivx, oiy = ofy * ivy, oiz = ofz * ivz;
       const float lo_c = round_down_f(-t_off);
       float hi_c = round_up_f(tlim - t_off);
       int sp = 0;
       const D3 c3 = d3(-rd.x, -rd.y, -rd.z);
 
       while (__ballot(cur != kDone) != 0) {
+        if (STATS) wave_tick(d_round_it, d_round_ln, lane);
+        if constexpr (WIDTH == 2) {
         while (!(cur & kLeaf)) {   // internal node (kDone carries the leaf bit)
-          if (STATS) c_nodes++;
+          if (STATS) { c_nodes++; wave_tick(d_node_it, d_node_ln, lane); }
           const float4* nq = reinterpret_cast<const float4*>(P.nodes + cur);
           const float4 bx = nq[0], by = nq[1], bz = nq[2];
           const uint2 rf = *reinterpret_cast<const uint2*>(nq + 3);
@@ -372,10 +406,54 @@ __global__ void __launch_bounds__(kBlock, 4) render_kernel(KParams P) {
             cur = (sp > 0) ? stk[--sp * kBlock] : kDone;
           }
         }
+        } else {
+        while (!(cur & kLeaf)) {   // 4-wide node: test 4 boxes, visit nearest, push the rest far-first
+          if (STATS) { c_nodes++; wave_tick(d_node_it, d_node_ln, lane); }
+          const char* nb = reinterpret_cast<const char*>(P.nodes4) + (size_t)cur * sizeof(GNode4);
+          const float4 nx = *reinterpret_cast<const float4*>(nb + nxo);
+          const float4 fx = *reinterpret_cast<const float4*>(nb + (nxo ^ 16u));
+          const float4 ny = *reinterpret_cast<const float4*>(nb + nyo);
+          const float4 fy = *reinterpret_cast<const float4*>(nb + (nyo ^ 16u));
+          const float4 nz = *reinterpret_cast<const float4*>(nb + nzo);
+          const float4 fz = *reinterpret_cast<const float4*>(nb + (nzo ^ 16u));
+          const uint4 rf = *reinterpret_cast<const uint4*>(nb + 96);
+          float k[4];
+          uint32_t v[4];
+          int cnt = 0;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const float tx0 = __builtin_fmaf(f4c(nx, c), ivx, -oix), tx1 = __builtin_fmaf(f4c(fx, c), ivx, -oix);
+            const float ty0 = __builtin_fmaf(f4c(ny, c), ivy, -oiy), ty1 = __builtin_fmaf(f4c(fy, c), ivy, -oiy);
+            const float tz0 = __builtin_fmaf(f4c(nz, c), ivz, -oiz), tz1 = __builtin_fmaf(f4c(fz, c), ivz, -oiz);
+            const float tn = fmaxf(fmaxf(tx0, ty0), fmaxf(tz0, lo_c));
+            const float tf = fminf(fminf(tx1, ty1), fminf(tz1, hi_c));
+            const uint32_t r = u4c(rf, c);
+            const bool h = (tn <= tf) && (r != kEmpty);
+            k[c] = h ? tn : INFINITY;
+            v[c] = r;
+            cnt += h ? 1 : 0;
+          }
+#define RT_CSWAP(a, b)                                        \
+  if (k[b] < k[a]) {                                          \
+    const float tk = k[a]; k[a] = k[b]; k[b] = tk;            \
+    const uint32_t tv = v[a]; v[a] = v[b]; v[b] = tv;         \
+  }
+          RT_CSWAP(0, 1) RT_CSWAP(2, 3) RT_CSWAP(0, 2) RT_CSWAP(1, 3) RT_CSWAP(1, 2)
+#undef RT_CSWAP
+          if (cnt == 0) {
+            cur = (sp > 0) ? stk[--sp * kBlock] : kDone;
+          } else {
+            if (cnt > 3) { stk[sp * kBlock] = v[3]; sp++; }
+            if (cnt > 2) { stk[sp * kBlock] = v[2]; sp++; }
+            if (cnt > 1) { stk[sp * kBlock] = v[1]; sp++; }
+            cur = v[0];
+          }
+        }
+        }
         if (cur != kDone) {   // leaf: test its triangles in slot order
           uint32_t i = cur & ~kLeaf;
           for (;;) {
-            if (STATS) c_tris++;
+            if (STATS) { c_tris++; wave_tick(d_leaf_it, d_leaf_ln, lane); }
             const TriOps T = load_tri(P.tris, i);
             // Mesh::intersect_triangle (mymesh.cpp:190-215), same values, early-outs reordered
             const D3 c4 = sub(ro, T.p2);
@@ -412,6 +490,7 @@ __global__ void __launch_bounds__(kBlock, 4) render_kernel(KParams P) {
       thit = tlim;
     }
     asm volatile("" ::: "memory");
+    if (STATS) { const unsigned long long t = stamp(); d_trav += t - t_stamp; t_stamp = t; }
 
     // ================= SHADE phase =================
     if (busy) {
@@ -551,6 +630,7 @@ __global__ void __launch_bounds__(kBlock, 4) render_kernel(KParams P) {
       }
     }
     asm volatile("" ::: "memory");
+    if (STATS) { const unsigned long long t = stamp(); d_shade += t - t_stamp; t_stamp = t; }
   }
 
   // ---------------- counters: one atomic per wave and counter ----------------
@@ -565,6 +645,22 @@ __global__ void __launch_bounds__(kBlock, 4) render_kernel(KParams P) {
       atomicAdd(&P.ctr[CS_NODES], s3);
       atomicAdd(&P.ctr[CS_TRIS], s4);
       atomicAdd(&P.ctr[CS_HITS], s5);
+      atomicAdd(&P.ctr[CD_TRAV_CYCLES], d_trav);     // wave-uniform values: lane 0's copy
+      atomicAdd(&P.ctr[CD_SHADE_CYCLES], d_shade);
+      atomicAdd(&P.ctr[CD_FETCH_CYCLES], d_fetch);
+      atomicAdd(&P.ctr[CD_OUTER_ITERS], d_outer);
+    }
+  }
+  if (STATS) {   // per-lane partial sums of the wave-level ticks
+    const unsigned long long a = wave_sum(d_node_it), b = wave_sum(d_node_ln), c = wave_sum(d_leaf_it);
+    const unsigned long long d = wave_sum(d_leaf_ln), e = wave_sum(d_round_it), f = wave_sum(d_round_ln);
+    if (lane == 0) {
+      atomicAdd(&P.ctr[CD_NODE_ITERS], a);
+      atomicAdd(&P.ctr[CD_NODE_LANES], b);
+      atomicAdd(&P.ctr[CD_LEAF_ITERS], c);
+      atomicAdd(&P.ctr[CD_LEAF_LANES], d);
+      atomicAdd(&P.ctr[CD_TRAV_ROUNDS], e);
+      atomicAdd(&P.ctr[CD_TRAV_ROUND_LANES], f);
     }
   }
 }
@@ -604,11 +700,14 @@ struct Variant {
   bool stats;
 };
 
+// [0] production (4-wide), [1] 4-wide + counters, [2] canonical 2-wide counters
+// (the traversal the oracle replicates: tests pin its node / triangle counts).
 const Variant kVariants[] = {
-    {render_kernel<false>, false},
-    {render_kernel<true>, true},
+    {render_kernel<4, false>, false},
+    {render_kernel<4, true>, true},
+    {render_kernel<2, true>, true},
 };
-constexpr int kNumVariants = 2;
+constexpr int kNumVariants = 3;
 constexpr int kMaxDepth = 128;   // LDS stack: depth * 256 threads * 4 B <= 128 KiB
 // LDS per block: 7 doubles of ray slot + stack_words u32 per thread.
 size_t lds_bytes(int stack_words) { return (size_t)kBlock * (7 * sizeof(double) + (size_t)stack_words * sizeof(uint32_t)); }
@@ -641,7 +740,9 @@ struct rt_scene {
   double root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};
   long long bytes = 0;
   int n_cu = 0;
-  int blocks_per_cu[kNumVariants] = {0, 0};
+  int blocks_per_cu[kNumVariants] = {0, 0, 0};
+  GNode4* d_nodes4 = nullptr;
+  int n_gnodes4 = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
 };
@@ -695,8 +796,8 @@ extern "C" {
 const char* rt_last_error(void) { return g_error.c_str(); }
 
 const char* rt_build_info(void) {
-  return "librt_hip: gfx950 persistent flattened render kernel; variants stats{0,1}; "
-         "fp32 2-wide nodes, fp64 triangles/shading, dynamic LDS stack, global path state, 8 XCD work heads";
+  return "librt_hip: gfx950 persistent flattened render kernel; variants {4-wide, 4-wide+stats, 2-wide canonical stats}; "
+         "fp32 4-wide nodes (128 B), fp64 triangles/shading, dynamic LDS stack, global path state, 8 XCD work heads";
 }
 
 int rt_scene_upload(const rt_scene_soa* s, const rt_bvh_soa* b, int device, rt_scene** out) {
@@ -761,8 +862,85 @@ int rt_scene_upload(const rt_scene_soa* s, const rt_bvh_soa* b, int device, rt_s
       }
     }
   }
-  if (depth > kMaxDepth)
-    return fail(RT_ERR_UNSUPPORTED, "rt_scene_upload: BVH deeper than 128 levels (LDS stack budget)");
+  // ---- 4-wide collapse of the same tree (production layout) ----
+  std::vector<GNode4> nodes4;
+  int stack4 = 1;
+  if (nt > 0) {
+    auto area = [&](int c) {
+      const double dx = b->bb_max[3 * (size_t)c] - b->bb_min[3 * (size_t)c];
+      const double dy = b->bb_max[3 * (size_t)c + 1] - b->bb_min[3 * (size_t)c + 1];
+      const double dz = b->bb_max[3 * (size_t)c + 2] - b->bb_min[3 * (size_t)c + 2];
+      return dx * dy + dy * dz + dz * dx;
+    };
+    auto kids_of = [&](int n) {   // open the largest internal child until 4 children
+      std::vector<int> k = {b->left_child[n], b->left_child[n] + 1};
+      while (k.size() < 4) {
+        int pick = -1;
+        double best_a = -1.0;
+        for (size_t i = 0; i < k.size(); ++i)
+          if (b->tri_count[k[i]] == 0 && area(k[i]) > best_a) { best_a = area(k[i]); pick = (int)i; }
+        if (pick < 0) break;
+        const int c = k[pick];
+        k[pick] = b->left_child[c];
+        k.insert(k.begin() + pick + 1, b->left_child[c] + 1);
+      }
+      return k;
+    };
+    auto set4 = [&](GNode4& g, int s_, int c) {
+      g.lox[s_] = round_down_host(b->bb_min[3 * (size_t)c] - delta);
+      g.hix[s_] = round_up_host(b->bb_max[3 * (size_t)c] + delta);
+      g.loy[s_] = round_down_host(b->bb_min[3 * (size_t)c + 1] - delta);
+      g.hiy[s_] = round_up_host(b->bb_max[3 * (size_t)c + 1] + delta);
+      g.loz[s_] = round_down_host(b->bb_min[3 * (size_t)c + 2] - delta);
+      g.hiz[s_] = round_up_host(b->bb_max[3 * (size_t)c + 2] + delta);
+    };
+    if (b->tri_count[0] > 0) {
+      GNode4 g;
+      std::memset(&g, 0, sizeof g);
+      set4(g, 0, 0);
+      g.ref[0] = kLeaf | (uint32_t)b->first_tri[0];
+      g.ref[1] = g.ref[2] = g.ref[3] = kEmpty;
+      nodes4.push_back(g);
+    } else {
+      std::vector<int> order;                  // reference ids of the collapsed nodes, preorder
+      std::vector<std::vector<int>> kids;
+      std::vector<int> g4(b->n_nodes, -1);
+      std::vector<int> stk = {0};
+      while (!stk.empty()) {
+        const int n = stk.back();
+        stk.pop_back();
+        g4[n] = (int)order.size();
+        order.push_back(n);
+        kids.push_back(kids_of(n));
+        const std::vector<int>& k = kids.back();
+        for (int i = (int)k.size() - 1; i >= 0; --i)
+          if (b->tri_count[k[i]] == 0) stk.push_back(k[i]);
+      }
+      nodes4.resize(order.size());
+      std::vector<int> need(order.size(), 0);   // stack entries needed below each node
+      for (int gi = (int)order.size() - 1; gi >= 0; --gi) {
+        GNode4& g = nodes4[gi];
+        std::memset(&g, 0, sizeof g);
+        const std::vector<int>& k = kids[gi];
+        int deeper = 0;
+        for (int s_ = 0; s_ < 4; ++s_) {
+          if (s_ < (int)k.size()) {
+            const int c = k[s_];
+            set4(g, s_, c);
+            g.ref[s_] = (b->tri_count[c] == 0) ? (uint32_t)g4[c] : (kLeaf | (uint32_t)b->first_tri[c]);
+            if (b->tri_count[c] == 0) deeper = std::max(deeper, need[g4[c]]);
+          } else {
+            g.ref[s_] = kEmpty;
+          }
+        }
+        need[gi] = (int)k.size() - 1 + deeper;
+      }
+      stack4 = std::max(1, need[0]);
+    }
+  }
+
+  if (depth > kMaxDepth || stack4 > kMaxDepth)
+    return fail(RT_ERR_UNSUPPORTED, "rt_scene_upload: BVH needs more than 128 stack entries (LDS budget)");
 
   // ---- triangle records / shading data in leaf order ----
   std::vector<GTri> tris((size_t)nt);
@@ -817,6 +995,7 @@ int rt_scene_upload(const rt_scene_soa* s, const rt_bvh_soa* b, int device, rt_s
   long long bytes = 0;
   rc = RT_OK;
   if (rc == RT_OK) rc = upload(&sc->d_nodes, nodes, bytes);
+  if (rc == RT_OK) rc = upload(&sc->d_nodes4, nodes4, bytes);
   if (rc == RT_OK) rc = upload(&sc->d_tris, tris, bytes);
   if (rc == RT_OK) rc = upload(&sc->d_shade, shade, bytes);
   if (rc == RT_OK) rc = upload(&sc->d_fnorm, fnorm, bytes);
@@ -837,7 +1016,8 @@ int rt_scene_upload(const rt_scene_soa* s, const rt_bvh_soa* b, int device, rt_s
   sc->n_tris = nt;
   sc->n_meshes = s->n_meshes;
   sc->depth = depth;
-  sc->stack_words = std::max(1, depth);
+  sc->stack_words = std::max(std::max(1, depth), stack4);
+  sc->n_gnodes4 = (int)nodes4.size();
   sc->delta = delta;
   if (nt > 0)
     for (int k = 0; k < 3; ++k) {
@@ -908,7 +1088,7 @@ int rt_launch_compute_image(rt_scene* sc, const rt_render_params* p, void* d_out
 
   KParams P;
   std::memset(&P, 0, sizeof P);
-  P.nodes = sc->d_nodes; P.tris = sc->d_tris; P.shade = sc->d_shade; P.fnorm = sc->d_fnorm;
+  P.nodes = sc->d_nodes; P.nodes4 = sc->d_nodes4; P.tris = sc->d_tris; P.shade = sc->d_shade; P.fnorm = sc->d_fnorm;
   P.vnorm = sc->d_vnorm; P.tu = sc->d_tu; P.tv = sc->d_tv; P.texels = sc->d_texels; P.mats = sc->d_mats;
   P.ctr = sc->d_ctr;
   P.out = d_out;
@@ -947,8 +1127,7 @@ int rt_launch_compute_image(rt_scene* sc, const rt_render_params* p, void* d_out
   P.tiles_x = (P.W + 7) / 8;
   P.n_tiles = (long long)P.tiles_x * ((rows + 7) / 8);
 
-  const bool want_stats = (p->flags & RT_FLAG_TRAVERSAL_STATS) != 0;
-  const int v = want_stats ? 1 : 0;
+  const int v = (p->flags & RT_FLAG_TRAVERSAL_STATS) ? 2 : ((p->flags & RT_FLAG_WIDE_STATS) ? 1 : 0);
   const size_t lds = lds_bytes(sc->stack_words);
   const long long waves_needed = (P.n_tiles * 64 + 63) / 64;
   long long blocks = (long long)sc->n_cu * sc->blocks_per_cu[v];
@@ -998,6 +1177,16 @@ int rt_render_to_host(rt_scene* sc, const rt_render_params* p, void* host_out, r
   return rc;
 }
 
+int rt_debug_counters(rt_scene* sc, unsigned long long* out, int n) {
+  if (!sc || !out || n <= 0) return fail(RT_ERR_INVALID, "rt_debug_counters: bad argument");
+  HIP_TRY(hipSetDevice(sc->device));
+  HIP_TRY(hipDeviceSynchronize());
+  unsigned long long c[kCtrWords];
+  HIP_TRY(hipMemcpy(c, sc->d_ctr, sizeof c, hipMemcpyDeviceToHost));
+  for (int i = 0; i < n && i < kCtrWords; ++i) out[i] = c[i];
+  return std::min(n, kCtrWords);
+}
+
 int rt_last_kernel_ms(rt_scene* sc, float* ms) {
   if (!sc || !ms || !sc->timed) return fail(RT_ERR_INVALID, "rt_last_kernel_ms: no launch recorded");
   HIP_TRY(hipEventSynchronize(sc->ev1));
@@ -1008,7 +1197,7 @@ int rt_last_kernel_ms(rt_scene* sc, float* ms) {
 void rt_scene_free(rt_scene* sc) {
   if (!sc) return;
   (void)hipSetDevice(sc->device);
-  void* ptrs[] = {sc->d_nodes, sc->d_tris, sc->d_shade, sc->d_fnorm, sc->d_vnorm, sc->d_tu,
+  void* ptrs[] = {sc->d_nodes, sc->d_nodes4, sc->d_tris, sc->d_shade, sc->d_fnorm, sc->d_vnorm, sc->d_tu,
                   sc->d_tv, sc->d_texels, sc->d_mats, sc->d_ctr, sc->d_pstate, sc->d_lights};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);

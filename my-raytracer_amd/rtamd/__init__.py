@@ -16,7 +16,7 @@ from pathlib import Path
 import numpy as np
 
 from . import abi
-from .abi import RT_OK, RT_OUT_RGB_F32, RT_OUT_RGB_F64, RT_FLAG_TRAVERSAL_STATS  # noqa: F401
+from .abi import RT_OK, RT_OUT_RGB_F32, RT_OUT_RGB_F64, RT_FLAG_TRAVERSAL_STATS, RT_FLAG_WIDE_STATS  # noqa: F401
 
 PKG_ROOT = Path(__file__).resolve().parent.parent
 LIB_DIR = PKG_ROOT / "lib"
@@ -213,6 +213,16 @@ class DeviceScene:
         _check_hip(hip_lib().rt_render_to_host(self._h, C.byref(params), img.ctypes.data_as(C.c_void_p),
                                                C.byref(st)), "rt_render_to_host")
         return img, st
+
+    def debug_counters(self):
+        """Raw counter words of the last launch (see rt_debug_counters in rt_hip.h)."""
+        buf = (C.c_ulonglong * 32)()
+        n = hip_lib().rt_debug_counters(self._h, buf, 32)
+        if n < 0:
+            _check_hip(n, "rt_debug_counters")
+        names = {16: "node_iters", 17: "node_lanes", 18: "leaf_iters", 19: "leaf_lanes", 20: "trav_cycles",
+                 21: "shade_cycles", 22: "fetch_cycles", 23: "outer_iters", 24: "trav_rounds", 25: "trav_round_lanes"}
+        return {v: int(buf[k]) for k, v in names.items()}
 
     def last_kernel_ms(self):
         ms = C.c_float(0.0)

@@ -17,6 +17,7 @@ RT_DRAW_PHONG = 1
 RT_OUT_RGB_F32 = 0
 RT_OUT_RGB_F64 = 1
 RT_FLAG_TRAVERSAL_STATS = 1
+RT_FLAG_WIDE_STATS = 2
 
 
 class Material(C.Structure):
@@ -120,6 +121,7 @@ HIP_SYMBOLS = {
                                           C.POINTER(Stats), C.c_void_p]),
     "rt_render_to_host": (C.c_int, [C.c_void_p, C.POINTER(RenderParams), C.c_void_p, C.POINTER(Stats)]),
     "rt_last_kernel_ms": (C.c_int, [C.c_void_p, C.POINTER(C.c_float)]),
+    "rt_debug_counters": (C.c_int, [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]),
     "rt_scene_free": (None, [C.c_void_p]),
     "rt_last_error": (C.c_char_p, []),
     "rt_build_info": (C.c_char_p, []),

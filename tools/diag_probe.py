@@ -1,0 +1,25 @@
+"""Diagnostic counters of the 4-wide traversal (dev tool): SIMD efficiency and phase cycle shares."""
+import sys
+
+sys.path.insert(0, "my-raytracer_amd")
+import rtamd  # noqa: E402
+
+kind = sys.argv[1] if len(sys.argv) > 1 else "office"
+w, h, spp = (int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])) if len(sys.argv) > 4 else (1920, 1080, 1)
+kw = {"n_triangles": 1000000} if kind == "random_tris" else {}
+host = rtamd.HostScene.generate(kind, **kw)
+host.prepare()
+gpu = rtamd.DeviceScene(host, 0)
+p = host.render_params(w, h, spp)
+for flags, name in [(rtamd.RT_FLAG_WIDE_STATS, "4-wide"), (rtamd.RT_FLAG_TRAVERSAL_STATS, "2-wide")]:
+    p.flags = flags
+    _, st = gpu.render(p)
+    d = gpu.debug_counters()
+    rays = st.primary_rays + st.shadow_rays + st.reflection_rays
+    tot = d["trav_cycles"] + d["shade_cycles"] + d["fetch_cycles"]
+    print(f"{kind} {w}x{h} {name}: rays {rays}  nodes/ray {st.node_visits/rays:.1f} tris/ray {st.tri_tests/rays:.1f}")
+    print(f"  node loop: {d['node_iters']} wave-iters, SIMD eff {d['node_lanes']/(64*max(1,d['node_iters'])):.3f}")
+    print(f"  leaf loop: {d['leaf_iters']} wave-iters, SIMD eff {d['leaf_lanes']/(64*max(1,d['leaf_iters'])):.3f}")
+    print(f"  trav rounds: {d['trav_rounds']}, lanes active {d['trav_round_lanes']/(64*max(1,d['trav_rounds'])):.3f}; outer iters {d['outer_iters']}")
+    print(f"  cycles: trav {d['trav_cycles']/tot:.3f} shade {d['shade_cycles']/tot:.3f} fetch {d['fetch_cycles']/tot:.3f} (total wave-cycles {tot:.3e})")
+    print(f"  per ray: node wave-iters {d['node_iters']*64/rays:.1f}  leaf wave-iters {d['leaf_iters']*64/rays:.1f}")

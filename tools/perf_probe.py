@@ -1,0 +1,32 @@
+"""Quick timing of the production kernel on several workloads (dev tool)."""
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, "my-raytracer_amd")
+import rtamd  # noqa: E402
+
+CASES = [("office", {}, 1920, 1080, 1), ("office", {}, 3840, 2160, 4), ("random_tris", {"n_triangles": 1000000}, 1920, 1080, 1)]
+if len(sys.argv) > 1 and sys.argv[1] == "quick":
+    CASES = CASES[:1]
+for kind, kw, w, h, spp in CASES:
+    t0 = time.time()
+    host = rtamd.HostScene.generate(kind, **kw)
+    bs = host.prepare()
+    gpu = rtamd.DeviceScene(host, 0)
+    p = host.render_params(w, h, spp)
+    img, st = gpu.render(p)
+    ms = []
+    for _ in range(5):
+        gpu.render(p)
+        ms.append(gpu.last_kernel_ms())
+    rays = st.primary_rays + st.shadow_rays + st.reflection_rays
+    p.flags = rtamd.RT_FLAG_WIDE_STATS
+    _, ws = gpu.render(p)
+    p.flags = rtamd.RT_FLAG_TRAVERSAL_STATS
+    _, cs = gpu.render(p)
+    m = float(np.median(ms))
+    print(f"{kind} {w}x{h} spp{spp*spp}: build {bs:.2f}s  kernel {m:.3f} ms  rays {rays}  {rays/m/1e3:.1f} Mrays/s  "
+          f"per-ray: wide nodes {ws.node_visits/rays:.1f} tris {ws.tri_tests/rays:.1f} | 2-wide nodes {cs.node_visits/rays:.1f} "
+          f"tris {cs.tri_tests/rays:.1f}  (total {time.time()-t0:.1f}s)", flush=True)
