@@ -197,8 +197,12 @@ __device__ __forceinline__ uint32_t u4c(const uint4& v, int c) {
   return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
 }
 
+#ifndef RT_WAVES_PER_EU
+#define RT_WAVES_PER_EU 4   // 4 waves/SIMD = 16 waves/CU (register budget 128 VGPRs)
+#endif
+
 template <int WIDTH, bool STATS>
-__global__ void __launch_bounds__(kBlock, 4) render_kernel(KParams P) {
+__global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   double* lds_d = reinterpret_cast<double*>(lds_raw);
   RaySlots R;
@@ -455,28 +459,41 @@ __global__ void __launch_bounds__(kBlock, 4) render_kernel(KParams P) {
           for (;;) {
             if (STATS) { c_tris++; wave_tick(d_leaf_it, d_leaf_ln, lane); }
             const TriOps T = load_tri(P.tris, i);
-            // Mesh::intersect_triangle (mymesh.cpp:190-215), same values, early-outs reordered
+            // Mesh::intersect_triangle (mymesh.cpp:190-215): the same fp64 S, Da, Db, Dt as
+            // the CPU (bit-identical operands and operation order).  Division-free early
+            // rejections first: they fire only where the CPU's rounded quotients certainly
+            // fail the same test (margins in DESIGN.md §4), so accept decisions are unchanged.
             const D3 c4 = sub(ro, T.p2);
             const double S = det3(T.e1, T.e2, c3);
             if (fabs(S) >= 1e-10) {
-              const double t = det3(T.e1, T.e2, c4) / S;
-              const bool cand = anyhit ? (t < tlim) : (t <= tlim);
-              if (t > 1e-5 && cand) {
-                const double alpha = det3(c4, T.e2, c3) / S;
-                const double beta = det3(T.e1, c4, c3) / S;
-                const double gamma = (1.0 - alpha - beta);
-                const bool inside = (0.0 <= alpha && alpha <= 1.0) && (0.0 <= beta && beta <= 1.0) &&
-                                    (0.0 <= gamma && gamma <= 1.0);
-                if (inside) {
-                  if (anyhit) {
-                    shadow_hit = true;
-                    cur = kDone;
-                    break;
-                  }
-                  if (t < tlim || (int)i < best) {   // ties: smallest slot (mybvh.cpp:169 visit order)
-                    tlim = t;
-                    best = (int)i;
-                    hi_c = round_up_f(tlim - t_off);
+              const double Da = det3(c4, T.e2, c3);
+              const double Db = det3(T.e1, c4, c3);
+              const double sS = S > 0.0 ? 1.0 : -1.0;
+              const double aS = fabs(S);
+              const double ua = Da * sS, ub = Db * sS;                       // sign-normalised numerators
+              const double tiny = aS * 0x1p-1000, big = aS * (1.0 + 0x1p-48);
+              const bool out = (ua < 0.0 && -ua >= tiny) || (ub < 0.0 && -ub >= tiny) || ua > big || ub > big ||
+                               (Da + Db - S) * sS > 0x1p-40 * (fabs(Da) + fabs(Db) + aS);
+              if (!out) {
+                const double t = det3(T.e1, T.e2, c4) / S;
+                const bool cand = anyhit ? (t < tlim) : (t <= tlim);
+                if (t > 1e-5 && cand) {
+                  const double alpha = Da / S;
+                  const double beta = Db / S;
+                  const double gamma = (1.0 - alpha - beta);
+                  const bool inside = (0.0 <= alpha && alpha <= 1.0) && (0.0 <= beta && beta <= 1.0) &&
+                                      (0.0 <= gamma && gamma <= 1.0);
+                  if (inside) {
+                    if (anyhit) {
+                      shadow_hit = true;
+                      cur = kDone;
+                      break;
+                    }
+                    if (t < tlim || (int)i < best) {   // ties: smallest slot (mybvh.cpp:169 visit order)
+                      tlim = t;
+                      best = (int)i;
+                      hi_c = round_up_f(tlim - t_off);
+                    }
                   }
                 }
               }

@@ -21,7 +21,7 @@ from .abi import RT_OK, RT_OUT_RGB_F32, RT_OUT_RGB_F64, RT_FLAG_TRAVERSAL_STATS,
 PKG_ROOT = Path(__file__).resolve().parent.parent
 LIB_DIR = PKG_ROOT / "lib"
 HOST_LIB = LIB_DIR / "librt_host.so"
-HIP_LIB = LIB_DIR / "librt_hip.so"
+HIP_LIB = Path(os.environ.get("RTAMD_HIP_LIB", LIB_DIR / "librt_hip.so"))   # override: kernel variants
 
 _host = None
 _hip = None
