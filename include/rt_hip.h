@@ -15,8 +15,9 @@
  *
  * Differences by design:
  *  - the scene is uploaded once with explicit hipMalloc/hipMemcpy into an
- *    MI355X layout (fp32 2-wide BVH nodes with child boxes in the parent,
- *    fp64 triangle records in leaf order); no managed memory;
+ *    MI355X layout (fp32 4-wide BVH nodes collapsed from the reference's
+ *    binary tree, child boxes in the parent; the 2-wide form for the canonical
+ *    counters; fp64 triangle records in leaf order); no managed memory;
  *  - the caller passes host SoA arrays (the reference's Data/BVHNodes_SoA
  *    content, same meaning, packed xyz instead of vec4) and owns the output;
  *  - errors are returned as status codes with the message in rt_last_error()
@@ -164,10 +165,11 @@ int rt_render_to_host(rt_scene* scene, const rt_render_params* p, void* host_out
 int rt_last_kernel_ms(rt_scene* scene, float* ms);
 
 /* Diagnostics: raw device counter words of the last launch (synchronises the
- * device).  Words [8,16) = rt_stats order; with a STATS flag, words [16,26) =
+ * device).  Words [8,16) = rt_stats order; with a STATS flag, words [16,27) =
  * node-loop iterations / active lanes, leaf-loop iterations / active lanes,
  * traverse / shade / refill cycles (s_memtime), outer iterations, traversal
- * rounds / active lanes (per wave, summed).  Returns the number of words copied. */
+ * rounds / active lanes (per wave, summed), traversal-stack entries spilled
+ * from the LDS ring to global memory.  Returns the number of words copied. */
 int rt_debug_counters(rt_scene* scene, unsigned long long* out, int n);
 
 void rt_scene_free(rt_scene* scene);

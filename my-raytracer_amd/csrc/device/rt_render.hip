@@ -48,6 +48,15 @@ constexpr int kBlock = 256;
 constexpr int kGroups = 8;          // work heads (XCD groups)
 constexpr int kRefill = 16;         // refill a wave when this many lanes are idle
 constexpr int kCtrWords = 32;       // [0,8) work heads, [8,16) stats, [16,32) diagnostics
+#ifndef RT_SHORT_STACK
+#define RT_SHORT_STACK 16
+#endif
+// Traversal stack: the top kShortStack entries live in an LDS ring (slot i & kStackMask),
+// deeper entries spill to a per-lane global array.  Bounds LDS per block independently
+// of tree depth, so occupancy stays VGPR-limited.
+constexpr int kShortStack = RT_SHORT_STACK;
+constexpr int kStackMask = kShortStack - 1;
+static_assert((kShortStack & kStackMask) == 0, "RT_SHORT_STACK must be a power of two");
 
 enum : int { ST_FETCH = 0, ST_CLOSEST = 1, ST_SHADOW = 2, ST_DONE = 3 };
 enum : int { CS_PRIMARY = 8, CS_SHADOW, CS_REFLECT, CS_NODES, CS_TRIS, CS_HITS, CS_PIXELS };
@@ -55,7 +64,7 @@ enum : int { CS_PRIMARY = 8, CS_SHADOW, CS_REFLECT, CS_NODES, CS_TRIS, CS_HITS, 
 // lanes summed over them (SIMD efficiency), s_memtime cycles per phase.
 enum : int {
   CD_NODE_ITERS = 16, CD_NODE_LANES, CD_LEAF_ITERS, CD_LEAF_LANES, CD_TRAV_CYCLES, CD_SHADE_CYCLES,
-  CD_FETCH_CYCLES, CD_OUTER_ITERS, CD_TRAV_ROUNDS, CD_TRAV_ROUND_LANES
+  CD_FETCH_CYCLES, CD_OUTER_ITERS, CD_TRAV_ROUNDS, CD_TRAV_ROUND_LANES, CD_SPILLS
 };
 
 struct KParams {
@@ -71,6 +80,7 @@ struct KParams {
   const GMat* mats;
   unsigned long long* ctr;
   double* pstate;       // [kFields][nslots] path state
+  uint32_t* spill;      // [stack_words][nslots] traversal-stack entries below the LDS ring
   const double* lights; // [n_lights][6] position xyz, colour rgb
   void* out;
   size_t nslots;
@@ -213,6 +223,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
   }
   R.tlim = lds_d + 6 * kBlock + threadIdx.x;
   uint32_t* stk = reinterpret_cast<uint32_t*>(lds_raw + 7 * kBlock * sizeof(double)) + threadIdx.x;
+  uint32_t* spill = P.spill + (size_t)blockIdx.x * kBlock + threadIdx.x;
 
   const int lane = threadIdx.x & 63;
   const unsigned long long lane_below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -236,6 +247,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
   unsigned long long c_nodes = 0, c_tris = 0;
   unsigned long long d_node_it = 0, d_node_ln = 0, d_leaf_it = 0, d_leaf_ln = 0;
   unsigned long long d_trav = 0, d_shade = 0, d_fetch = 0, d_outer = 0, d_round_it = 0, d_round_ln = 0;
+  unsigned long long d_spills = 0;
   unsigned long long t_stamp = 0;
   auto stamp = [&]() -> unsigned long long { return STATS ? __builtin_amdgcn_s_memtime() : 0ull; };
 
@@ -374,7 +386,24 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
       const float oix = ofx * ivx, oiy = ofy * ivy, oiz = ofz * ivz;
       const float lo_c = round_down_f(-t_off);
       float hi_c = round_up_f(tlim - t_off);
-      int sp = 0;
+      // logical stack [0, sp); the LDS ring holds [slo, sp), spill[] holds [0, slo)
+      int sp = 0, slo = 0;
+      auto push = [&](uint32_t x) {
+        if (sp - slo == kShortStack) {
+          spill[(size_t)slo * P.nslots] = stk[(slo & kStackMask) * kBlock];
+          slo++;
+          if (STATS) d_spills++;
+        }
+        stk[(sp & kStackMask) * kBlock] = x;
+        sp++;
+      };
+      auto pop = [&]() -> uint32_t {
+        if (sp == 0) return kDone;
+        --sp;
+        if (sp >= slo) return stk[(sp & kStackMask) * kBlock];
+        slo = sp;
+        return spill[(size_t)sp * P.nslots];
+      };
       const D3 c3 = d3(-rd.x, -rd.y, -rd.z);
 
       while (__ballot(cur != kDone) != 0) {
@@ -399,15 +428,14 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
           const bool h1 = (tn1 <= tf1) && (rf.y != kEmpty);
           if (h0 && h1) {
             const bool swap = tn1 < tn0;
-            stk[sp * kBlock] = swap ? rf.x : rf.y;
-            sp++;
+            push(swap ? rf.x : rf.y);
             cur = swap ? rf.y : rf.x;
           } else if (h0) {
             cur = rf.x;
           } else if (h1) {
             cur = rf.y;
           } else {
-            cur = (sp > 0) ? stk[--sp * kBlock] : kDone;
+            cur = pop();
           }
         }
         } else {
@@ -445,11 +473,11 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
           RT_CSWAP(0, 1) RT_CSWAP(2, 3) RT_CSWAP(0, 2) RT_CSWAP(1, 3) RT_CSWAP(1, 2)
 #undef RT_CSWAP
           if (cnt == 0) {
-            cur = (sp > 0) ? stk[--sp * kBlock] : kDone;
+            cur = pop();
           } else {
-            if (cnt > 3) { stk[sp * kBlock] = v[3]; sp++; }
-            if (cnt > 2) { stk[sp * kBlock] = v[2]; sp++; }
-            if (cnt > 1) { stk[sp * kBlock] = v[1]; sp++; }
+            if (cnt > 3) push(v[3]);
+            if (cnt > 2) push(v[2]);
+            if (cnt > 1) push(v[1]);
             cur = v[0];
           }
         }
@@ -501,7 +529,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
             if (T.last) break;
             ++i;
           }
-          if (cur != kDone) cur = (sp > 0) ? stk[--sp * kBlock] : kDone;
+          if (cur != kDone) cur = pop();
         }
       }
       thit = tlim;
@@ -671,6 +699,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
   if (STATS) {   // per-lane partial sums of the wave-level ticks
     const unsigned long long a = wave_sum(d_node_it), b = wave_sum(d_node_ln), c = wave_sum(d_leaf_it);
     const unsigned long long d = wave_sum(d_leaf_ln), e = wave_sum(d_round_it), f = wave_sum(d_round_ln);
+    const unsigned long long g = wave_sum(d_spills);
     if (lane == 0) {
       atomicAdd(&P.ctr[CD_NODE_ITERS], a);
       atomicAdd(&P.ctr[CD_NODE_LANES], b);
@@ -678,6 +707,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
       atomicAdd(&P.ctr[CD_LEAF_LANES], d);
       atomicAdd(&P.ctr[CD_TRAV_ROUNDS], e);
       atomicAdd(&P.ctr[CD_TRAV_ROUND_LANES], f);
+      atomicAdd(&P.ctr[CD_SPILLS], g);
     }
   }
 }
@@ -725,9 +755,11 @@ const Variant kVariants[] = {
     {render_kernel<2, true>, true},
 };
 constexpr int kNumVariants = 3;
-constexpr int kMaxDepth = 128;   // LDS stack: depth * 256 threads * 4 B <= 128 KiB
-// LDS per block: 7 doubles of ray slot + stack_words u32 per thread.
-size_t lds_bytes(int stack_words) { return (size_t)kBlock * (7 * sizeof(double) + (size_t)stack_words * sizeof(uint32_t)); }
+constexpr int kMaxDepth = 4096;  // traversal stack entries (LDS ring + global spill)
+// LDS per block: 7 doubles of ray slot + min(stack_words, kShortStack) u32 per thread.
+size_t lds_bytes(int stack_words) {
+  return (size_t)kBlock * (7 * sizeof(double) + (size_t)std::min(stack_words, kShortStack) * sizeof(uint32_t));
+}
 
 }  // namespace
 
@@ -749,6 +781,7 @@ struct rt_scene {
   int depth = 0;
   int stack_words = 1;          // LDS stack entries per thread (>= tree depth)
   double* d_pstate = nullptr;   // [kFields][nslots]
+  uint32_t* d_spill = nullptr;  // [stack_words][nslots] (only when stack_words > kShortStack)
   size_t nslots = 0;
   double* d_lights = nullptr;   // [RT_MAX_LIGHTS][6]
   int cached_lights = -1;       // light count currently in d_lights
@@ -957,7 +990,7 @@ int rt_scene_upload(const rt_scene_soa* s, const rt_bvh_soa* b, int device, rt_s
   }
 
   if (depth > kMaxDepth || stack4 > kMaxDepth)
-    return fail(RT_ERR_UNSUPPORTED, "rt_scene_upload: BVH needs more than 128 stack entries (LDS budget)");
+    return fail(RT_ERR_UNSUPPORTED, "rt_scene_upload: BVH needs more than 4096 traversal-stack entries");
 
   // ---- triangle records / shading data in leaf order ----
   std::vector<GTri> tris((size_t)nt);
@@ -1062,6 +1095,14 @@ int rt_scene_upload(const rt_scene_soa* s, const rt_bvh_soa* b, int device, rt_s
     return fail(RT_ERR_HIP, "hipMalloc of path state failed");
   }
   sc->bytes += (long long)(sc->nslots * kFields * sizeof(double) + RT_MAX_LIGHTS * 6 * sizeof(double));
+  if (sc->stack_words > kShortStack) {
+    const size_t sb = sc->nslots * (size_t)sc->stack_words * sizeof(uint32_t);
+    if (hipMalloc(reinterpret_cast<void**>(&sc->d_spill), sb) != hipSuccess) {
+      rt_scene_free(sc);
+      return fail(RT_ERR_HIP, "hipMalloc of traversal-stack spill failed");
+    }
+    sc->bytes += (long long)sb;
+  }
   if (hipEventCreate(&sc->ev0) != hipSuccess || hipEventCreate(&sc->ev1) != hipSuccess) {
     rt_scene_free(sc);
     return fail(RT_ERR_HIP, "hipEventCreate failed");
@@ -1134,6 +1175,7 @@ int rt_launch_compute_image(rt_scene* sc, const rt_render_params* p, void* d_out
   }
   P.lights = sc->d_lights;
   P.pstate = sc->d_pstate;
+  P.spill = sc->d_spill;
   P.nslots = sc->nslots;
   P.spp_n = p->spp_n;
   P.row_begin = scount == 1 ? std::max(0, p->row_begin) : 0;
@@ -1215,7 +1257,7 @@ void rt_scene_free(rt_scene* sc) {
   if (!sc) return;
   (void)hipSetDevice(sc->device);
   void* ptrs[] = {sc->d_nodes, sc->d_nodes4, sc->d_tris, sc->d_shade, sc->d_fnorm, sc->d_vnorm, sc->d_tu,
-                  sc->d_tv, sc->d_texels, sc->d_mats, sc->d_ctr, sc->d_pstate, sc->d_lights};
+                  sc->d_tv, sc->d_texels, sc->d_mats, sc->d_ctr, sc->d_pstate, sc->d_lights, sc->d_spill};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   if (sc->ev0) (void)hipEventDestroy(sc->ev0);

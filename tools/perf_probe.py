@@ -10,6 +10,12 @@ import rtamd  # noqa: E402
 CASES = [("office", {}, 1920, 1080, 1), ("office", {}, 3840, 2160, 4), ("random_tris", {"n_triangles": 1000000}, 1920, 1080, 1)]
 if len(sys.argv) > 1 and sys.argv[1] == "quick":
     CASES = CASES[:1]
+elif len(sys.argv) > 1 and sys.argv[1] != "all":   # kind:WxH:spp_n[:n_triangles] ...
+    CASES = []
+    for spec in sys.argv[1:]:
+        f = spec.split(":")
+        w, h = map(int, f[1].split("x"))
+        CASES.append((f[0], {"n_triangles": int(f[3])} if len(f) > 3 else {}, w, h, int(f[2])))
 for kind, kw, w, h, spp in CASES:
     t0 = time.time()
     host = rtamd.HostScene.generate(kind, **kw)
@@ -24,9 +30,10 @@ for kind, kw, w, h, spp in CASES:
     rays = st.primary_rays + st.shadow_rays + st.reflection_rays
     p.flags = rtamd.RT_FLAG_WIDE_STATS
     _, ws = gpu.render(p)
+    spills = gpu.debug_counters()["stack_spills"]
     p.flags = rtamd.RT_FLAG_TRAVERSAL_STATS
     _, cs = gpu.render(p)
     m = float(np.median(ms))
     print(f"{kind} {w}x{h} spp{spp*spp}: build {bs:.2f}s  kernel {m:.3f} ms  rays {rays}  {rays/m/1e3:.1f} Mrays/s  "
           f"per-ray: wide nodes {ws.node_visits/rays:.1f} tris {ws.tri_tests/rays:.1f} | 2-wide nodes {cs.node_visits/rays:.1f} "
-          f"tris {cs.tri_tests/rays:.1f}  (total {time.time()-t0:.1f}s)", flush=True)
+          f"tris {cs.tri_tests/rays:.1f}  spills/ray {spills/rays:.4f}  (total {time.time()-t0:.1f}s)", flush=True)
