@@ -165,11 +165,12 @@ int rt_render_to_host(rt_scene* scene, const rt_render_params* p, void* host_out
 int rt_last_kernel_ms(rt_scene* scene, float* ms);
 
 /* Diagnostics: raw device counter words of the last launch (synchronises the
- * device).  Words [8,16) = rt_stats order; with a STATS flag, words [16,27) =
+ * device).  Words [8,16) = rt_stats order; with a STATS flag, words [16,30) =
  * node-loop iterations / active lanes, leaf-loop iterations / active lanes,
  * traverse / shade / refill cycles (s_memtime), outer iterations, traversal
  * rounds / active lanes (per wave, summed), traversal-stack entries spilled
- * from the LDS ring to global memory.  Returns the number of words copied. */
+ * from the LDS ring to global memory, distinct nodes / triangle lines per
+ * wave-level node / leaf iteration (summed), triangle tests in leaves of > 4.  Returns the number of words copied. */
 int rt_debug_counters(rt_scene* scene, unsigned long long* out, int n);
 
 void rt_scene_free(rt_scene* scene);

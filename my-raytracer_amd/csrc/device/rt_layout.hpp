@@ -13,9 +13,10 @@
 //    numbered in depth-first preorder (left child = parent + 1).
 //    ref: internal child -> its GNode index; leaf child -> LEAF | first slot;
 //    EMPTY marks the absent sibling of a single-leaf root.
-//  * GTri (80 B): fp64 triangle record in leaf order, holding exactly the
-//    operands of the reference's Cramer test (mymesh.cpp:190-193):
-//    e1 = p0 - p2, e2 = p1 - p2, p2, plus mesh id and an end-of-leaf flag.
+//  * GTri (80 B): fp64 triangle record in device leaf order, holding exactly
+//    the operands of the reference's Cramer test (mymesh.cpp:190-193):
+//    e1 = p0 - p2, e2 = p1 - p2, p2, plus mesh id, reference slot and
+//    end-of-leaf flags.
 //  * Shading data is only touched once per closest hit: per-slot vertex /
 //    uv indices, face normals, vertex normals, uvs, texels, materials.
 #pragma once
@@ -50,12 +51,20 @@ struct alignas(128) GNode4 {
 };
 static_assert(sizeof(GNode4) == 128, "GNode4 must be 128 bytes");
 
+// GTri.meta: reference leaf slot (the tie-break key and the 2-wide iteration
+// order) plus two end-of-leaf flags.  Records sit in DEVICE order: the reference
+// leaf order, except that oversize reference leaves are refined into sub-leaves
+// whose triangles are permuted within the leaf's slot range.
+constexpr uint32_t kSlotMask = 0x3fffffffu;
+constexpr uint32_t kLastRef = 0x40000000u;   // slot is the last of its reference leaf
+constexpr uint32_t kLastDev = 0x80000000u;   // record is the last of its device leaf
+
 struct alignas(16) GTri {
   double e1[3];
   double e2[3];
   double p2[3];
   int32_t mesh;
-  uint32_t last;   // 1 = last triangle of its leaf
+  uint32_t meta;   // slot | kLastRef | kLastDev
 };
 static_assert(sizeof(GTri) == 80, "GTri must be 80 bytes");
 

@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cfloat>
 #include <cmath>
 #include <cstdio>
@@ -46,7 +47,10 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kGroups = 8;          // work heads (XCD groups)
-constexpr int kRefill = 16;         // refill a wave when this many lanes are idle
+#ifndef RT_REFILL
+#define RT_REFILL 16
+#endif
+constexpr int kRefill = RT_REFILL;  // refill a wave when this many lanes are idle
 constexpr int kCtrWords = 32;       // [0,8) work heads, [8,16) stats, [16,32) diagnostics
 #ifndef RT_SHORT_STACK
 #define RT_SHORT_STACK 16
@@ -64,13 +68,15 @@ enum : int { CS_PRIMARY = 8, CS_SHADOW, CS_REFLECT, CS_NODES, CS_TRIS, CS_HITS, 
 // lanes summed over them (SIMD efficiency), s_memtime cycles per phase.
 enum : int {
   CD_NODE_ITERS = 16, CD_NODE_LANES, CD_LEAF_ITERS, CD_LEAF_LANES, CD_TRAV_CYCLES, CD_SHADE_CYCLES,
-  CD_FETCH_CYCLES, CD_OUTER_ITERS, CD_TRAV_ROUNDS, CD_TRAV_ROUND_LANES, CD_SPILLS
+  CD_FETCH_CYCLES, CD_OUTER_ITERS, CD_TRAV_ROUNDS, CD_TRAV_ROUND_LANES, CD_SPILLS, CD_NODE_LINES,
+  CD_LEAF_LINES, CD_BIG_LEAF_TESTS
 };
 
 struct KParams {
   const GNode* nodes;
   const GNode4* nodes4;
   const GTri* tris;
+  const uint32_t* slot2dev; // reference slot -> device record (2-wide canonical kernel)
   const TriShade* shade;
   const double* fnorm;
   const double* vnorm;
@@ -159,10 +165,24 @@ __device__ __forceinline__ void wave_tick(unsigned long long& iters, unsigned lo
   if (lane == __ffsll((long long)m) - 1) { iters++; lanes += __popcll(m); }
 }
 
+// Adds the number of distinct keys among the active lanes (wave-uniform loop) on the
+// first active lane: distinct lines one load instruction touches, the L1 tag rate's unit.
+__device__ __forceinline__ void wave_distinct(uint32_t key, unsigned long long& acc, int lane) {
+  unsigned long long m = __ballot(1);
+  const int first = __ffsll((long long)m) - 1;
+  unsigned n = 0;
+  while (m) {
+    const uint32_t k = __shfl(key, __ffsll((long long)m) - 1);
+    m &= ~__ballot(key == k);
+    n++;
+  }
+  if (lane == first) acc += n;
+}
+
 struct TriOps {
   D3 e1, e2, p2;
   int mesh;
-  uint32_t last;
+  uint32_t meta;
 };
 __device__ __forceinline__ TriOps load_tri(const GTri* tris, uint32_t i) {
   const double2* q = reinterpret_cast<const double2*>(tris + i);
@@ -173,7 +193,7 @@ __device__ __forceinline__ TriOps load_tri(const GTri* tris, uint32_t i) {
   T.p2 = d3(d.x, d.y, e.x);
   const int2 meta = *reinterpret_cast<const int2*>(&q[4].y);
   T.mesh = meta.x;
-  T.last = (uint32_t)meta.y;
+  T.meta = (uint32_t)meta.y;
   return T;
 }
 
@@ -240,14 +260,15 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
   // ---- per-lane state live across phases ----
   int state = ST_FETCH;
   int px = 0, lrow = 0, py = 0, sample = 0, depth = 0, light = 0, mesh = 0;
-  int best = kNoHit;
+  int best = kNoHit;        // device record of the closest hit
+  int best_slot = kNoHit;   // its reference slot (tie-break key)
   double thit = DBL_MAX;
   bool shadow_hit = false;
   unsigned c_primary = 0, c_shadow = 0, c_refl = 0, c_hits = 0;
   unsigned long long c_nodes = 0, c_tris = 0;
   unsigned long long d_node_it = 0, d_node_ln = 0, d_leaf_it = 0, d_leaf_ln = 0;
   unsigned long long d_trav = 0, d_shade = 0, d_fetch = 0, d_outer = 0, d_round_it = 0, d_round_ln = 0;
-  unsigned long long d_spills = 0;
+  unsigned long long d_spills = 0, d_node_lines = 0, d_leaf_lines = 0, d_big_leaf = 0;
   unsigned long long t_stamp = 0;
   auto stamp = [&]() -> unsigned long long { return STATS ? __builtin_amdgcn_s_memtime() : 0ull; };
 
@@ -334,6 +355,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
       const D3 rd = d3(*R.d[0], *R.d[1], *R.d[2]);
       double tlim = *R.tlim;
       best = kNoHit;
+      best_slot = kNoHit;
       shadow_hit = false;
       uint32_t cur = kDone;
       double t_off = 0.0;
@@ -410,7 +432,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
         if (STATS) wave_tick(d_round_it, d_round_ln, lane);
         if constexpr (WIDTH == 2) {
         while (!(cur & kLeaf)) {   // internal node (kDone carries the leaf bit)
-          if (STATS) { c_nodes++; wave_tick(d_node_it, d_node_ln, lane); }
+          if (STATS) { c_nodes++; wave_tick(d_node_it, d_node_ln, lane); wave_distinct(cur, d_node_lines, lane); }
           const float4* nq = reinterpret_cast<const float4*>(P.nodes + cur);
           const float4 bx = nq[0], by = nq[1], bz = nq[2];
           const uint2 rf = *reinterpret_cast<const uint2*>(nq + 3);
@@ -440,7 +462,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
         }
         } else {
         while (!(cur & kLeaf)) {   // 4-wide node: test 4 boxes, visit nearest, push the rest far-first
-          if (STATS) { c_nodes++; wave_tick(d_node_it, d_node_ln, lane); }
+          if (STATS) { c_nodes++; wave_tick(d_node_it, d_node_ln, lane); wave_distinct(cur, d_node_lines, lane); }
           const char* nb = reinterpret_cast<const char*>(P.nodes4) + (size_t)cur * sizeof(GNode4);
           const float4 nx = *reinterpret_cast<const float4*>(nb + nxo);
           const float4 fx = *reinterpret_cast<const float4*>(nb + (nxo ^ 16u));
@@ -483,10 +505,20 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
         }
         }
         if (cur != kDone) {   // leaf: test its triangles in slot order
+          // 2-wide: iterate reference slots in order (the oracle's order); 4-wide: device
+          // records of the (possibly refined) leaf.  Either way the hit kept is the
+          // smallest (t, slot), which does not depend on the order.
           uint32_t i = cur & ~kLeaf;
+          const uint32_t leaf0 = i;
           for (;;) {
-            if (STATS) { c_tris++; wave_tick(d_leaf_it, d_leaf_ln, lane); }
-            const TriOps T = load_tri(P.tris, i);
+            const uint32_t rec = (WIDTH == 2) ? P.slot2dev[i] : i;
+            if (STATS) {
+              c_tris++;
+              wave_tick(d_leaf_it, d_leaf_ln, lane);
+              wave_distinct((uint32_t)(((unsigned long long)i * sizeof(GTri)) >> 7), d_leaf_lines, lane);
+            }
+            const TriOps T = load_tri(P.tris, rec);
+            const int slot = (int)(T.meta & kSlotMask);
             // Mesh::intersect_triangle (mymesh.cpp:190-215): the same fp64 S, Da, Db, Dt as
             // the CPU (bit-identical operands and operation order).  Division-free early
             // rejections first: they fire only where the CPU's rounded quotients certainly
@@ -517,18 +549,20 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
                       cur = kDone;
                       break;
                     }
-                    if (t < tlim || (int)i < best) {   // ties: smallest slot (mybvh.cpp:169 visit order)
+                    if (t < tlim || slot < best_slot) {   // ties: smallest slot (mybvh.cpp:169 visit order)
                       tlim = t;
-                      best = (int)i;
+                      best = (int)rec;
+                      best_slot = slot;
                       hi_c = round_up_f(tlim - t_off);
                     }
                   }
                 }
               }
             }
-            if (T.last) break;
+            if (T.meta & (WIDTH == 2 ? kLastRef : kLastDev)) break;
             ++i;
           }
+          if (STATS && i - leaf0 + 1 > 4) d_big_leaf += i - leaf0 + 1;
           if (cur != kDone) cur = pop();
         }
       }
@@ -699,7 +733,8 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
   if (STATS) {   // per-lane partial sums of the wave-level ticks
     const unsigned long long a = wave_sum(d_node_it), b = wave_sum(d_node_ln), c = wave_sum(d_leaf_it);
     const unsigned long long d = wave_sum(d_leaf_ln), e = wave_sum(d_round_it), f = wave_sum(d_round_ln);
-    const unsigned long long g = wave_sum(d_spills);
+    const unsigned long long g = wave_sum(d_spills), h = wave_sum(d_node_lines), q = wave_sum(d_leaf_lines);
+    const unsigned long long r = wave_sum(d_big_leaf);
     if (lane == 0) {
       atomicAdd(&P.ctr[CD_NODE_ITERS], a);
       atomicAdd(&P.ctr[CD_NODE_LANES], b);
@@ -708,6 +743,9 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
       atomicAdd(&P.ctr[CD_TRAV_ROUNDS], e);
       atomicAdd(&P.ctr[CD_TRAV_ROUND_LANES], f);
       atomicAdd(&P.ctr[CD_SPILLS], g);
+      atomicAdd(&P.ctr[CD_NODE_LINES], h);
+      atomicAdd(&P.ctr[CD_LEAF_LINES], q);
+      atomicAdd(&P.ctr[CD_BIG_LEAF_TESTS], r);
     }
   }
 }
@@ -767,6 +805,7 @@ struct rt_scene {
   int device = 0;
   GNode* d_nodes = nullptr;
   GTri* d_tris = nullptr;
+  uint32_t* d_slot2dev = nullptr;
   TriShade* d_shade = nullptr;
   double* d_fnorm = nullptr;
   double* d_vnorm = nullptr;
@@ -808,11 +847,105 @@ int upload(T** dst, const std::vector<T>& src, long long& bytes) {
   return RT_OK;
 }
 
+#ifndef RT_LEAF_MAX
+#define RT_LEAF_MAX 2
+#endif
+constexpr int kLeafMax = RT_LEAF_MAX;   // device leaves hold at most this many triangles
+
+// Binary tree the device layouts are built from: the reference tree (mybvh.cpp)
+// node for node, with reference leaves of more than kLeafMax triangles refined.
+struct DevTree {
+  std::vector<std::array<double, 3>> lo, hi;
+  std::vector<int> left, right;    // internal: children (device-tree ids)
+  std::vector<int> first, count;   // count > 0: leaf of device records [first, first + count)
+  int add() {
+    lo.push_back({0, 0, 0});
+    hi.push_back({0, 0, 0});
+    left.push_back(-1);
+    right.push_back(-1);
+    first.push_back(0);
+    count.push_back(0);
+    return (int)left.size() - 1;
+  }
+};
+
+void build_device_tree(const rt_scene_soa* s, const rt_bvh_soa* b, DevTree& E, std::vector<uint32_t>& dev2slot) {
+  const long long nt = s->n_vertex_idx / 3;
+  for (long long i = 0; i < nt; ++i) dev2slot[i] = (uint32_t)i;
+  auto vtx = [&](uint32_t slot, int c) { return s->vertex_pos + 3 * (size_t)s->vertex_idx[3 * (size_t)slot + c]; };
+  auto centroid = [&](uint32_t slot, int k) { return (vtx(slot, 0)[k] + vtx(slot, 1)[k] + vtx(slot, 2)[k]) / 3.0; };
+  // refines device records [first, first + count) under node id (explicit work list)
+  struct Job { int id, first, count; };
+  std::vector<Job> jobs;
+  auto refine = [&](int root, int first0, int count0) {
+    jobs.push_back({root, first0, count0});
+    while (!jobs.empty()) {
+      const Job j = jobs.back();
+      jobs.pop_back();
+      std::array<double, 3> lo = {DBL_MAX, DBL_MAX, DBL_MAX}, hi = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
+      std::array<double, 3> clo = lo, chi = hi;
+      for (int r = j.first; r < j.first + j.count; ++r)
+        for (int k = 0; k < 3; ++k) {
+          for (int c = 0; c < 3; ++c) {
+            lo[k] = std::min(lo[k], vtx(dev2slot[r], c)[k]);
+            hi[k] = std::max(hi[k], vtx(dev2slot[r], c)[k]);
+          }
+          clo[k] = std::min(clo[k], centroid(dev2slot[r], k));
+          chi[k] = std::max(chi[k], centroid(dev2slot[r], k));
+        }
+      E.lo[j.id] = lo;
+      E.hi[j.id] = hi;
+      if (j.count <= kLeafMax) {
+        E.first[j.id] = j.first;
+        E.count[j.id] = j.count;
+        continue;
+      }
+      int axis = 0;
+      for (int k = 1; k < 3; ++k)
+        if (chi[k] - clo[k] > chi[axis] - clo[axis]) axis = k;
+      if (chi[axis] > clo[axis])   // median of centroids on the longest axis (else: halve in slot order)
+        std::stable_sort(dev2slot.begin() + j.first, dev2slot.begin() + j.first + j.count,
+                         [&](uint32_t a, uint32_t c) { return centroid(a, axis) < centroid(c, axis); });
+      const int l = E.add(), r = E.add();
+      E.left[j.id] = l;
+      E.right[j.id] = r;
+      const int half = j.count / 2;
+      jobs.push_back({r, j.first + half, j.count - half});
+      jobs.push_back({l, j.first, half});
+    }
+  };
+  // reference tree, node for node (explicit stack: reference depth is unbounded)
+  std::vector<std::pair<int, int>> stk;   // (reference node, device-tree id)
+  stk.emplace_back(0, E.add());
+  while (!stk.empty()) {
+    const auto [n, id] = stk.back();
+    stk.pop_back();
+    for (int k = 0; k < 3; ++k) {
+      E.lo[id][k] = b->bb_min[3 * (size_t)n + k];
+      E.hi[id][k] = b->bb_max[3 * (size_t)n + k];
+    }
+    if (b->tri_count[n] == 0) {
+      const int l = E.add(), r = E.add();
+      E.left[id] = l;
+      E.right[id] = r;
+      stk.emplace_back(b->left_child[n] + 1, r);
+      stk.emplace_back(b->left_child[n], l);
+    } else if (b->tri_count[n] <= kLeafMax) {
+      E.first[id] = b->first_tri[n];
+      E.count[id] = b->tri_count[n];
+    } else {
+      refine(id, b->first_tri[n], b->tri_count[n]);
+    }
+  }
+}
+
 int validate(const rt_scene_soa* s, const rt_bvh_soa* b) {
   if (!s || !b) return fail(RT_ERR_INVALID, "rt_scene_upload: null scene or bvh");
   if (s->n_vertex_idx % 3 != 0 || s->n_vertex_idx < 0 || s->n_vertices < 0 || s->n_meshes < 0)
     return fail(RT_ERR_INVALID, "rt_scene_upload: inconsistent counts");
   const long long nt = s->n_vertex_idx / 3;
+  if (nt > (long long)kSlotMask)
+    return fail(RT_ERR_UNSUPPORTED, "rt_scene_upload: more than 2^30 triangles");
   if (nt > 0 && (b->n_nodes < 1 || b->n_nodes > 2 * nt - 1))
     return fail(RT_ERR_INVALID, "rt_scene_upload: bvh node count out of range");
   for (long long i = 0; i < s->n_vertex_idx; ++i)
@@ -912,49 +1045,60 @@ int rt_scene_upload(const rt_scene_soa* s, const rt_bvh_soa* b, int device, rt_s
       }
     }
   }
-  // ---- 4-wide collapse of the same tree (production layout) ----
+  // ---- device binary tree: the reference tree with oversize leaves refined ----
+  // Reference leaves of more than kLeafMax triangles (coplanar grids the fixed-axis
+  // median split cannot separate, mybvh.cpp:95-130) get a sub-tree split on the
+  // longest centroid axis; their triangles are permuted within the leaf's slot
+  // range.  The closest hit is the smallest (t, slot) over a conservative superset
+  // of the triangles the ray can hit, so it does not depend on the tree.
+  DevTree E;
+  std::vector<uint32_t> dev2slot((size_t)std::max<long long>(nt, 1));
+  if (nt > 0) build_device_tree(s, b, E, dev2slot);
+  std::vector<uint32_t> slot2dev((size_t)std::max<long long>(nt, 1), 0);
+  for (long long g = 0; g < nt; ++g) slot2dev[dev2slot[g]] = (uint32_t)g;
+
+  // ---- 4-wide collapse of the device tree (production layout) ----
   std::vector<GNode4> nodes4;
   int stack4 = 1;
   if (nt > 0) {
     auto area = [&](int c) {
-      const double dx = b->bb_max[3 * (size_t)c] - b->bb_min[3 * (size_t)c];
-      const double dy = b->bb_max[3 * (size_t)c + 1] - b->bb_min[3 * (size_t)c + 1];
-      const double dz = b->bb_max[3 * (size_t)c + 2] - b->bb_min[3 * (size_t)c + 2];
+      const double dx = E.hi[c][0] - E.lo[c][0], dy = E.hi[c][1] - E.lo[c][1], dz = E.hi[c][2] - E.lo[c][2];
       return dx * dy + dy * dz + dz * dx;
     };
+    auto internal = [&](int c) { return E.count[c] == 0; };
     auto kids_of = [&](int n) {   // open the largest internal child until 4 children
-      std::vector<int> k = {b->left_child[n], b->left_child[n] + 1};
+      std::vector<int> k = {E.left[n], E.right[n]};
       while (k.size() < 4) {
         int pick = -1;
         double best_a = -1.0;
         for (size_t i = 0; i < k.size(); ++i)
-          if (b->tri_count[k[i]] == 0 && area(k[i]) > best_a) { best_a = area(k[i]); pick = (int)i; }
+          if (internal(k[i]) && area(k[i]) > best_a) { best_a = area(k[i]); pick = (int)i; }
         if (pick < 0) break;
         const int c = k[pick];
-        k[pick] = b->left_child[c];
-        k.insert(k.begin() + pick + 1, b->left_child[c] + 1);
+        k[pick] = E.left[c];
+        k.insert(k.begin() + pick + 1, E.right[c]);
       }
       return k;
     };
     auto set4 = [&](GNode4& g, int s_, int c) {
-      g.lox[s_] = round_down_host(b->bb_min[3 * (size_t)c] - delta);
-      g.hix[s_] = round_up_host(b->bb_max[3 * (size_t)c] + delta);
-      g.loy[s_] = round_down_host(b->bb_min[3 * (size_t)c + 1] - delta);
-      g.hiy[s_] = round_up_host(b->bb_max[3 * (size_t)c + 1] + delta);
-      g.loz[s_] = round_down_host(b->bb_min[3 * (size_t)c + 2] - delta);
-      g.hiz[s_] = round_up_host(b->bb_max[3 * (size_t)c + 2] + delta);
+      g.lox[s_] = round_down_host(E.lo[c][0] - delta);
+      g.hix[s_] = round_up_host(E.hi[c][0] + delta);
+      g.loy[s_] = round_down_host(E.lo[c][1] - delta);
+      g.hiy[s_] = round_up_host(E.hi[c][1] + delta);
+      g.loz[s_] = round_down_host(E.lo[c][2] - delta);
+      g.hiz[s_] = round_up_host(E.hi[c][2] + delta);
     };
-    if (b->tri_count[0] > 0) {
+    if (!internal(0)) {
       GNode4 g;
       std::memset(&g, 0, sizeof g);
       set4(g, 0, 0);
-      g.ref[0] = kLeaf | (uint32_t)b->first_tri[0];
+      g.ref[0] = kLeaf | (uint32_t)E.first[0];
       g.ref[1] = g.ref[2] = g.ref[3] = kEmpty;
       nodes4.push_back(g);
     } else {
-      std::vector<int> order;                  // reference ids of the collapsed nodes, preorder
+      std::vector<int> order;                  // device-tree ids of the collapsed nodes, preorder
       std::vector<std::vector<int>> kids;
-      std::vector<int> g4(b->n_nodes, -1);
+      std::vector<int> g4(E.left.size(), -1);
       std::vector<int> stk = {0};
       while (!stk.empty()) {
         const int n = stk.back();
@@ -964,7 +1108,7 @@ int rt_scene_upload(const rt_scene_soa* s, const rt_bvh_soa* b, int device, rt_s
         kids.push_back(kids_of(n));
         const std::vector<int>& k = kids.back();
         for (int i = (int)k.size() - 1; i >= 0; --i)
-          if (b->tri_count[k[i]] == 0) stk.push_back(k[i]);
+          if (internal(k[i])) stk.push_back(k[i]);
       }
       nodes4.resize(order.size());
       std::vector<int> need(order.size(), 0);   // stack entries needed below each node
@@ -977,8 +1121,8 @@ int rt_scene_upload(const rt_scene_soa* s, const rt_bvh_soa* b, int device, rt_s
           if (s_ < (int)k.size()) {
             const int c = k[s_];
             set4(g, s_, c);
-            g.ref[s_] = (b->tri_count[c] == 0) ? (uint32_t)g4[c] : (kLeaf | (uint32_t)b->first_tri[c]);
-            if (b->tri_count[c] == 0) deeper = std::max(deeper, need[g4[c]]);
+            g.ref[s_] = internal(c) ? (uint32_t)g4[c] : (kLeaf | (uint32_t)E.first[c]);
+            if (internal(c)) deeper = std::max(deeper, need[g4[c]]);
           } else {
             g.ref[s_] = kEmpty;
           }
@@ -992,23 +1136,28 @@ int rt_scene_upload(const rt_scene_soa* s, const rt_bvh_soa* b, int device, rt_s
   if (depth > kMaxDepth || stack4 > kMaxDepth)
     return fail(RT_ERR_UNSUPPORTED, "rt_scene_upload: BVH needs more than 4096 traversal-stack entries");
 
-  // ---- triangle records / shading data in leaf order ----
+  // ---- triangle records / shading data in device order ----
+  std::vector<uint8_t> last_dev((size_t)std::max<long long>(nt, 1), 0);
+  for (size_t n = 0; n < E.left.size(); ++n)
+    if (E.count[n] > 0) last_dev[(size_t)E.first[n] + E.count[n] - 1] = 1;
   std::vector<GTri> tris((size_t)nt);
   std::vector<TriShade> shade((size_t)nt);
-  for (long long i = 0; i < nt; ++i) {
+  std::vector<double> fnorm(3 * (size_t)nt);
+  for (long long g = 0; g < nt; ++g) {
+    const long long i = dev2slot[g];   // reference slot
     const int v0 = s->vertex_idx[3 * i], v1 = s->vertex_idx[3 * i + 1], v2 = s->vertex_idx[3 * i + 2];
     const double* p0 = s->vertex_pos + 3 * (size_t)v0;
     const double* p1 = s->vertex_pos + 3 * (size_t)v1;
     const double* p2 = s->vertex_pos + 3 * (size_t)v2;
-    GTri& T = tris[i];
+    GTri& T = tris[g];
     for (int k = 0; k < 3; ++k) {
       T.e1[k] = p0[k] - p2[k];
       T.e2[k] = p1[k] - p2[k];
       T.p2[k] = p2[k];
     }
     T.mesh = s->vertex_mesh_id[v0];                 // meshId = vertexMeshId_[vi0], mytracer_gpu.cu:492
-    T.last = last[i];
-    TriShade& sh = shade[i];
+    T.meta = (uint32_t)i | (last[i] ? kLastRef : 0u) | (last_dev[g] ? kLastDev : 0u);
+    TriShade& sh = shade[g];
     sh.v[0] = v0; sh.v[1] = v1; sh.v[2] = v2;
     for (int k = 0; k < 3; ++k) sh.t[k] = s->texture_idx ? s->texture_idx[3 * i + k] : -1;
     sh.pad[0] = sh.pad[1] = 0;
@@ -1016,6 +1165,7 @@ int rt_scene_upload(const rt_scene_soa* s, const rt_bvh_soa* b, int device, rt_s
       for (int k = 0; k < 3; ++k)
         if (sh.t[k] < 0 || sh.t[k] >= s->n_tex_coords)
           return fail(RT_ERR_INVALID, "rt_scene_upload: textured mesh with invalid uv index");
+    for (int k = 0; k < 3; ++k) fnorm[3 * (size_t)g + k] = s->face_normals[3 * i + k];
   }
   std::vector<GMat> mats((size_t)s->n_meshes);
   for (int m = 0; m < s->n_meshes; ++m) {
@@ -1034,7 +1184,6 @@ int rt_scene_upload(const rt_scene_soa* s, const rt_bvh_soa* b, int device, rt_s
     G.tex_h = s->mesh_tex_height[m];
     G.tex_off = s->mesh_tex_offset[m];
   }
-  std::vector<double> fnorm(s->face_normals, s->face_normals + 3 * nt);
   std::vector<double> vnorm(s->vertex_normals, s->vertex_normals + 3 * (size_t)s->n_vertices);
   std::vector<double> tu(s->tex_u, s->tex_u + s->n_tex_coords), tv(s->tex_v, s->tex_v + s->n_tex_coords);
   std::vector<unsigned char> texels(s->texels, s->texels + 3 * s->n_texels);
@@ -1047,6 +1196,7 @@ int rt_scene_upload(const rt_scene_soa* s, const rt_bvh_soa* b, int device, rt_s
   if (rc == RT_OK) rc = upload(&sc->d_nodes, nodes, bytes);
   if (rc == RT_OK) rc = upload(&sc->d_nodes4, nodes4, bytes);
   if (rc == RT_OK) rc = upload(&sc->d_tris, tris, bytes);
+  if (rc == RT_OK) rc = upload(&sc->d_slot2dev, slot2dev, bytes);
   if (rc == RT_OK) rc = upload(&sc->d_shade, shade, bytes);
   if (rc == RT_OK) rc = upload(&sc->d_fnorm, fnorm, bytes);
   if (rc == RT_OK) rc = upload(&sc->d_vnorm, vnorm, bytes);
@@ -1146,7 +1296,7 @@ int rt_launch_compute_image(rt_scene* sc, const rt_render_params* p, void* d_out
 
   KParams P;
   std::memset(&P, 0, sizeof P);
-  P.nodes = sc->d_nodes; P.nodes4 = sc->d_nodes4; P.tris = sc->d_tris; P.shade = sc->d_shade; P.fnorm = sc->d_fnorm;
+  P.nodes = sc->d_nodes; P.nodes4 = sc->d_nodes4; P.tris = sc->d_tris; P.slot2dev = sc->d_slot2dev; P.shade = sc->d_shade; P.fnorm = sc->d_fnorm;
   P.vnorm = sc->d_vnorm; P.tu = sc->d_tu; P.tv = sc->d_tv; P.texels = sc->d_texels; P.mats = sc->d_mats;
   P.ctr = sc->d_ctr;
   P.out = d_out;
@@ -1257,7 +1407,8 @@ void rt_scene_free(rt_scene* sc) {
   if (!sc) return;
   (void)hipSetDevice(sc->device);
   void* ptrs[] = {sc->d_nodes, sc->d_nodes4, sc->d_tris, sc->d_shade, sc->d_fnorm, sc->d_vnorm, sc->d_tu,
-                  sc->d_tv, sc->d_texels, sc->d_mats, sc->d_ctr, sc->d_pstate, sc->d_lights, sc->d_spill};
+                  sc->d_tv, sc->d_texels, sc->d_mats, sc->d_ctr, sc->d_pstate, sc->d_lights, sc->d_spill,
+                  sc->d_slot2dev};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   if (sc->ev0) (void)hipEventDestroy(sc->ev0);

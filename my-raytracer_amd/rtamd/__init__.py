@@ -222,7 +222,7 @@ class DeviceScene:
             _check_hip(n, "rt_debug_counters")
         names = {16: "node_iters", 17: "node_lanes", 18: "leaf_iters", 19: "leaf_lanes", 20: "trav_cycles",
                  21: "shade_cycles", 22: "fetch_cycles", 23: "outer_iters", 24: "trav_rounds", 25: "trav_round_lanes",
-                 26: "stack_spills"}
+                 26: "stack_spills", 27: "node_lines", 28: "leaf_lines", 29: "big_leaf_tests"}
         return {v: int(buf[k]) for k, v in names.items()}
 
     def last_kernel_ms(self):

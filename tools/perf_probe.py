@@ -30,10 +30,14 @@ for kind, kw, w, h, spp in CASES:
     rays = st.primary_rays + st.shadow_rays + st.reflection_rays
     p.flags = rtamd.RT_FLAG_WIDE_STATS
     _, ws = gpu.render(p)
-    spills = gpu.debug_counters()["stack_spills"]
+    dc = gpu.debug_counters()
+    spills = dc["stack_spills"]
+    diag = (f"  node: simd {dc['node_lanes']/max(1,dc['node_iters']):.1f} lanes, {dc['node_lines']/max(1,dc['node_iters']):.1f} lines"
+            f" | leaf: simd {dc['leaf_lanes']/max(1,dc['leaf_iters']):.1f}, {dc['leaf_lines']/max(1,dc['leaf_iters']):.1f} lines"
+            f" | big-leaf tests {dc['big_leaf_tests']/max(1,ws.tri_tests):.2f} | iters/ray node {dc['node_iters']*64/rays:.1f} leaf {dc['leaf_iters']*64/rays:.1f}")
     p.flags = rtamd.RT_FLAG_TRAVERSAL_STATS
     _, cs = gpu.render(p)
     m = float(np.median(ms))
     print(f"{kind} {w}x{h} spp{spp*spp}: build {bs:.2f}s  kernel {m:.3f} ms  rays {rays}  {rays/m/1e3:.1f} Mrays/s  "
           f"per-ray: wide nodes {ws.node_visits/rays:.1f} tris {ws.tri_tests/rays:.1f} | 2-wide nodes {cs.node_visits/rays:.1f} "
-          f"tris {cs.tri_tests/rays:.1f}  spills/ray {spills/rays:.4f}  (total {time.time()-t0:.1f}s)", flush=True)
+          f"tris {cs.tri_tests/rays:.1f}  spills/ray {spills/rays:.4f}  (total {time.time()-t0:.1f}s)\n   {diag}", flush=True)
