@@ -173,6 +173,12 @@ int rt_last_kernel_ms(rt_scene* scene, float* ms);
  * wave-level node / leaf iteration (summed), triangle tests in leaves of > 4.  Returns the number of words copied. */
 int rt_debug_counters(rt_scene* scene, unsigned long long* out, int n);
 
+/* Diagnostics: per-wave timeline of the last launch with a STATS flag: words
+ * [4w, 4w+4) of wave w of the persistent grid = {start, last successful work
+ * fetch, end} (s_memrealtime, 100 MHz) and pixels fetched; waves that were not
+ * launched keep stale words.  Synchronises the device; returns words copied. */
+long long rt_debug_wave_log(rt_scene* scene, unsigned long long* out, long long n);
+
 void rt_scene_free(rt_scene* scene);
 
 /* Thread-local message of the last failing call. */

@@ -62,7 +62,36 @@ constexpr int kShortStack = RT_SHORT_STACK;
 constexpr int kStackMask = kShortStack - 1;
 static_assert((kShortStack & kStackMask) == 0, "RT_SHORT_STACK must be a power of two");
 
-enum : int { ST_FETCH = 0, ST_CLOSEST = 1, ST_SHADOW = 2, ST_DONE = 3 };
+// Lane states.  Owners carry a pixel (CLOSEST: closest-hit ray in flight; SHADOW: a
+// batch of shadow rays in flight).  Idle lanes (FETCH / DONE) may be lent to an
+// owner of the same wave for one round (HSHADOW / HCLOSEST): they trace one of its
+// extra shadow rays or its reflection ray, so a bounce costs one round, not 1 + lights.
+enum : int { ST_FETCH = 0, ST_CLOSEST = 1, ST_SHADOW = 2, ST_DONE = 3, ST_HSHADOW = 4, ST_HCLOSEST = 5 };
+#ifndef RT_FANOUT
+#define RT_FANOUT 2   // 0: off, 1: extra shadow rays, 2: + reflection ray
+#endif
+constexpr uint32_t kTaskNone = 0xffffffffu;
+constexpr uint32_t kTaskRefl = 0x10000u;   // task word: owner lane | light << 8 | kTaskRefl
+
+// Orders LDS traffic between lanes of one wave: LDS executes a wave's operations in
+// issue order, so it suffices to stop the compiler from moving memory operations
+// across this point and to drain outstanding LDS operations.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Lane of the k-th (0-based) set bit of m (k < popcount(m)).
+__device__ __forceinline__ int kth_set_bit(unsigned long long m, int k) {
+  int base = 0;
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) {
+    const int c = __popcll(m & ((1ull << w) - 1ull));
+    if (k >= c) { k -= c; m >>= w; base += w; }
+  }
+  return base;
+}
 enum : int { CS_PRIMARY = 8, CS_SHADOW, CS_REFLECT, CS_NODES, CS_TRIS, CS_HITS, CS_PIXELS };
 // diagnostics (STATS variants only): wave-level loop iterations and the active
 // lanes summed over them (SIMD efficiency), s_memtime cycles per phase.
@@ -87,6 +116,7 @@ struct KParams {
   unsigned long long* ctr;
   double* pstate;       // [kFields][nslots] path state
   uint32_t* spill;      // [stack_words][nslots] traversal-stack entries below the LDS ring
+  unsigned long long* wavelog;  // STATS: per wave {start, last refill, end, pixels} (s_memrealtime)
   const double* lights; // [n_lights][6] position xyz, colour rgb
   void* out;
   size_t nslots;
@@ -201,7 +231,7 @@ __device__ __forceinline__ TriOps load_tri(const GTri* tris, uint32_t i) {
 // persistent grid.  They are touched only when a ray completes.
 enum : int {
   F_PCOL = 0, F_SCOL = 3, F_W = 6, F_HP = 7, F_HN = 10, F_HVIEW = 13, F_HDIFF = 16,
-  F_LACC = 19, F_CONTRIB = 22, F_MIRROR = 25, kFields = 28
+  F_LACC = 19, F_MIRROR = 22, kFields = 23
 };
 
 // LDS ray slots ([field][thread], conflict-free): the only hand-over between
@@ -242,7 +272,10 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
     R.d[k] = lds_d + (3 + k) * kBlock + threadIdx.x;
   }
   R.tlim = lds_d + 6 * kBlock + threadIdx.x;
-  uint32_t* stk = reinterpret_cast<uint32_t*>(lds_raw + 7 * kBlock * sizeof(double)) + threadIdx.x;
+  uint32_t* ltask = reinterpret_cast<uint32_t*>(lds_raw + 7 * kBlock * sizeof(double));   // [kBlock]
+  uint32_t* lvis = ltask + kBlock;                                                             // [kBlock]
+  uint32_t* stk = lvis + kBlock + threadIdx.x;
+  const int wbase = threadIdx.x & ~63;   // first thread of this wave
   uint32_t* spill = P.spill + (size_t)blockIdx.x * kBlock + threadIdx.x;
 
   const int lane = threadIdx.x & 63;
@@ -264,11 +297,16 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
   int best_slot = kNoHit;   // its reference slot (tie-break key)
   double thit = DBL_MAX;
   bool shadow_hit = false;
+  int batch_end = 0;      // owner: lights [light, batch_end) in flight
+  int refl_h = -1;        // owner: lane tracing its reflection ray this round (-1: none)
+  int want = 0;           // owner: extra rays it would lend lanes for
+  uint32_t htask = kTaskNone;   // helper: its task word
   unsigned c_primary = 0, c_shadow = 0, c_refl = 0, c_hits = 0;
   unsigned long long c_nodes = 0, c_tris = 0;
   unsigned long long d_node_it = 0, d_node_ln = 0, d_leaf_it = 0, d_leaf_ln = 0;
   unsigned long long d_trav = 0, d_shade = 0, d_fetch = 0, d_outer = 0, d_round_it = 0, d_round_ln = 0;
   unsigned long long d_spills = 0, d_node_lines = 0, d_leaf_lines = 0, d_big_leaf = 0;
+  unsigned long long w_start = STATS ? __builtin_amdgcn_s_memrealtime() : 0ull, w_refill = 0, w_pixels = 0;
   unsigned long long t_stamp = 0;
   auto stamp = [&]() -> unsigned long long { return STATS ? __builtin_amdgcn_s_memtime() : 0ull; };
 
@@ -302,7 +340,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
     if (STATS) { d_outer++; t_stamp = stamp(); }
     // ---------------- refill idle lanes (one atomic per wave) ----------------
     unsigned long long m_fetch = __ballot(state == ST_FETCH);
-    unsigned long long m_busy = __ballot(state == ST_CLOSEST || state == ST_SHADOW);
+    unsigned long long m_busy = __ballot(state == ST_CLOSEST || state == ST_SHADOW || state >= ST_HSHADOW);
     while (m_fetch && (__popcll(m_fetch) >= kRefill || m_busy == 0) && heads_left > 0) {
       const long long g0 = (P.n_tiles * head / kGroups) * 64;
       const long long g1 = (P.n_tiles * (head + 1) / kGroups) * 64;
@@ -317,6 +355,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
         heads_left--;
         continue;
       }
+      if (STATS) { w_refill = __builtin_amdgcn_s_memrealtime(); w_pixels += (unsigned long long)min((long long)cnt, g1 - start); }
       if (state == ST_FETCH) {
         const long long wk = start + __popcll(m_fetch & lane_below);
         if (wk < g1) {
@@ -337,11 +376,11 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
         }
       }
       m_fetch = __ballot(state == ST_FETCH);
-      m_busy = __ballot(state == ST_CLOSEST || state == ST_SHADOW);
+      m_busy = __ballot(state == ST_CLOSEST || state == ST_SHADOW || state >= ST_HSHADOW);
       if (__popcll(m_fetch) < kRefill && m_busy != 0) break;
     }
     if (heads_left == 0 && state == ST_FETCH) state = ST_DONE;
-    const bool busy = (state == ST_CLOSEST || state == ST_SHADOW);
+    const bool busy = (state == ST_CLOSEST || state == ST_SHADOW || state >= ST_HSHADOW);
     if (__ballot(busy) == 0) {
       if (__ballot(state != ST_DONE) == 0) break;
       continue;
@@ -350,7 +389,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
     if (STATS) { const unsigned long long t = stamp(); d_fetch += t - t_stamp; t_stamp = t; }
     // ================= TRAVERSE phase =================
     {
-      const bool anyhit = (state == ST_SHADOW);
+      const bool anyhit = (state == ST_SHADOW || state == ST_HSHADOW);
       const D3 ro = d3(*R.o[0], *R.o[1], *R.o[2]);
       const D3 rd = d3(*R.d[0], *R.d[1], *R.d[2]);
       double tlim = *R.tlim;
@@ -571,12 +610,101 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
     asm volatile("" ::: "memory");
     if (STATS) { const unsigned long long t = stamp(); d_trav += t - t_stamp; t_stamp = t; }
 
-    // ================= SHADE phase =================
-    if (busy) {
-      bool lights_phase = false, fresh_hit = false, finish = false;
-      D3 hp = d3(0, 0, 0), hn = d3(0, 0, 0), hview = d3(0, 0, 0), hdiff = d3(0, 0, 0), lacc = d3(0, 0, 0);
+    // ---- helpers hand their result to the owner, then go idle ----
+    {
+      const int idle_state = heads_left > 0 ? ST_FETCH : ST_DONE;
+      if (state == ST_HSHADOW) {
+        if (shadow_hit) atomicOr(&lvis[wbase + (int)(htask & 63u)], 1u << ((htask >> 8) & 31u));
+        state = idle_state;
+      } else if (state == ST_HCLOSEST) {
+        ltask[threadIdx.x] = (uint32_t)best;
+        *R.tlim = thit;
+        state = idle_state;
+      }
+      wave_lds_sync();
+    }
+
+    // ================= SHADE phase (owners) =================
+    want = 0;
+    if (state == ST_CLOSEST || state == ST_SHADOW) {
+      bool hit_ready = (state == ST_CLOSEST), finish = false;
+      D3 hp, hn, hview;
       double mirror = 0.0;
-      if (state == ST_CLOSEST) {
+      // lighting() for one light (mytracer.cpp:579-606): Lambert + Phong term of light j
+      auto contrib_of = [&](int j, D3 hp_, D3 hn_, D3 hv_, D3 hd_, const GMat& M) {
+        const double* L6 = P.lights + 6 * j;
+        const D3 l = normalize(sub(d3(L6[0], L6[1], L6[2]), hp_));
+        const double diff = stdmax(0.0, dot(hn_, l));
+        double refl = 0.0;
+        if (diff > 0.0) {   // reflection(), mytracer.cpp:524-534
+          const double s2 = 2.0 * dot(hn_, l);
+          const D3 r = normalize(sub(scl(s2, hn_), l));
+          refl = stdmax(0.0, dot(r, hv_));
+        }
+        refl = pow(refl, M.shininess);
+        return d3(L6[3] * (hd_.x * diff + M.ks[0] * refl), L6[4] * (hd_.y * diff + M.ks[1] * refl),
+                  L6[5] * (hd_.z * diff + M.ks[2] * refl));
+      };
+      // own shadow ray for light `light`; the rest of the bounce is offered to idle lanes
+      auto launch_batch = [&](D3 hp_, double mirror_) {
+        const double* L6 = P.lights + 6 * light;
+        const D3 to_l = sub(d3(L6[0], L6[1], L6[2]), hp_);
+        const D3 l = normalize(to_l);
+        c_shadow++;
+        emit_ray(add(hp_, scl(1e-4, l)), l, sqrt(dot(to_l, to_l)));
+        state = ST_SHADOW;
+        lvis[threadIdx.x] = 0u;
+        batch_end = light + 1;
+        refl_h = -1;
+        want = RT_FANOUT == 0 ? 0
+               : (P.n_lights - light - 1) + ((RT_FANOUT > 1 && mirror_ > 0.0 && depth < P.max_depth) ? 1 : 0);
+      };
+      if (state == ST_SHADOW) {   // batch finished: lights [light, batch_end) in order
+        hp = LD3(F_HP); hn = LD3(F_HN); hview = LD3(F_HVIEW);
+        const D3 hdiff = LD3(F_HDIFF);
+        mirror = LD(F_MIRROR);
+        D3 lacc = LD3(F_LACC);
+        const GMat& M = P.mats[mesh];
+        const uint32_t vw = lvis[threadIdx.x];
+        for (int j = light; j < batch_end; ++j) {
+          const bool occluded = (j == light) ? shadow_hit : (((vw >> j) & 1u) != 0u);
+          const D3 c = contrib_of(j, hp, hn, hview, hdiff, M);
+          if (!occluded) lacc = add(lacc, c);
+        }
+        light = batch_end;
+        if (light < P.n_lights) {
+          ST3(F_LACC, lacc);
+          launch_batch(hp, mirror);
+        } else {   // bounce complete (subtrace, mytracer.cpp:546-555)
+          const double w = LD(F_W);
+          ST3(F_SCOL, add(LD3(F_SCOL), scl(w, scl(1.0 - mirror, lacc))));
+          if (mirror > 0.0 && depth < P.max_depth) {
+            ST(F_W, w * mirror);
+            depth++;
+            if (refl_h >= 0) {   // reflection ray traced by a helper this round
+              const int ht = wbase + refl_h;
+#pragma unroll
+              for (int k = 0; k < 3; ++k) {
+                *R.o[k] = lds_d[k * kBlock + ht];
+                *R.d[k] = lds_d[(3 + k) * kBlock + ht];
+              }
+              best = (int)ltask[ht];
+              thit = lds_d[6 * kBlock + ht];
+              hit_ready = true;
+            } else {
+              const D3 d = d3(-hview.x, -hview.y, -hview.z);   // reflect(d, n) = d - 2(n.d)n
+              const double s2 = 2.0 * dot(hn, d);
+              const D3 v = sub(d, scl(s2, hn));
+              c_refl++;
+              emit_ray(add(hp, scl(1e-4, v)), v, DBL_MAX);
+              state = ST_CLOSEST;
+            }
+          } else {
+            finish = true;
+          }
+        }
+      }
+      if (hit_ready) {
         if (best == kNoHit) {   // miss: background (mytracer_gpu.cu:262, :292)
           ST3(F_SCOL, add(LD3(F_SCOL), scl(LD(F_W), d3(P.bg[0], P.bg[1], P.bg[2]))));
           finish = true;
@@ -608,6 +736,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
             hn = d3(alpha * n0[0] + beta * n1[0] + gamma * n2[0], alpha * n0[1] + beta * n1[1] + gamma * n2[1],
                     alpha * n0[2] + beta * n1[2] + gamma * n2[2]);
           }
+          D3 hdiff;
           if (M.tex_w > 0) {
             const TriShade sh = P.shade[best];
             double u = alpha * P.tu[sh.t[0]] + beta * P.tu[sh.t[1]] + gamma * P.tu[sh.t[2]];
@@ -623,67 +752,29 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
             hdiff = d3(M.kd[0], M.kd[1], M.kd[2]);
           }
           // ambient term (mytracer.cpp:574-576)
-          lacc = d3(0.0 + P.amb[0] * M.ka[0], 0.0 + P.amb[1] * M.ka[1], 0.0 + P.amb[2] * M.ka[2]);
+          D3 lacc = d3(0.0 + P.amb[0] * M.ka[0], 0.0 + P.amb[1] * M.ka[1], 0.0 + P.amb[2] * M.ka[2]);
           light = 0;
-          lights_phase = true;
-          fresh_hit = true;
-        }
-      } else {   // shadow ray of light `light` finished (mytracer.cpp:599-605)
-        lacc = LD3(F_LACC);
-        if (!shadow_hit) lacc = add(lacc, LD3(F_CONTRIB));
-        light++;
-        hp = LD3(F_HP); hn = LD3(F_HN); hview = LD3(F_HVIEW); hdiff = LD3(F_HDIFF);
-        mirror = LD(F_MIRROR);
-        lights_phase = true;
-      }
-      if (lights_phase) {
-        const GMat& M = P.mats[mesh];
-        bool launched = false;
-        while (light < P.n_lights) {   // mytracer.cpp:579-606
-          const double* L6 = P.lights + 6 * light;
-          const D3 to_l = sub(d3(L6[0], L6[1], L6[2]), hp);
-          const D3 l = normalize(to_l);
-          const double diff = stdmax(0.0, dot(hn, l));
-          double refl = 0.0;
-          if (diff > 0.0) {   // reflection(), mytracer.cpp:524-534
-            const double s = 2.0 * dot(hn, l);
-            const D3 r = normalize(sub(scl(s, hn), l));
-            refl = stdmax(0.0, dot(r, hview));
-          }
-          refl = pow(refl, M.shininess);
-          const D3 contrib = d3(L6[3] * (hdiff.x * diff + M.ks[0] * refl), L6[4] * (hdiff.y * diff + M.ks[1] * refl),
-                                L6[5] * (hdiff.z * diff + M.ks[2] * refl));
-          if (M.shadowable) {   // shadow ray, mytracer.cpp:589-600
-            if (fresh_hit) {
-              ST3(F_HP, hp); ST3(F_HN, hn); ST3(F_HVIEW, hview); ST3(F_HDIFF, hdiff);
-              ST(F_MIRROR, mirror);
-            }
+          if (M.shadowable && P.n_lights > 0) {   // shadow rays, mytracer.cpp:589-600
+            ST3(F_HP, hp); ST3(F_HN, hn); ST3(F_HVIEW, hview); ST3(F_HDIFF, hdiff);
+            ST(F_MIRROR, mirror);
             ST3(F_LACC, lacc);
-            ST3(F_CONTRIB, contrib);
-            c_shadow++;
-            emit_ray(add(hp, scl(1e-4, l)), l, sqrt(dot(to_l, to_l)));
-            state = ST_SHADOW;
-            launched = true;
-            break;
-          }
-          lacc = add(lacc, contrib);
-          light++;
-        }
-        if (!launched) {
-          // all lights done; reflect only if mirror > 0 (subtrace, mytracer.cpp:546-555)
-          const double w = LD(F_W);
-          ST3(F_SCOL, add(LD3(F_SCOL), scl(w, scl(1.0 - mirror, lacc))));
-          if (mirror > 0.0 && depth < P.max_depth) {
-            ST(F_W, w * mirror);
-            depth++;
-            const D3 d = d3(-hview.x, -hview.y, -hview.z);   // direction of the ray that hit
-            const double s = 2.0 * dot(hn, d);               // reflect(d, n) = d - 2(n.d)n
-            const D3 v = sub(d, scl(s, hn));
-            c_refl++;
-            emit_ray(add(hp, scl(1e-4, v)), v, DBL_MAX);
-            state = ST_CLOSEST;
+            launch_batch(hp, mirror);
           } else {
-            finish = true;
+            for (int j = 0; j < P.n_lights; ++j) lacc = add(lacc, contrib_of(j, hp, hn, hview, hdiff, M));
+            const double w = LD(F_W);
+            ST3(F_SCOL, add(LD3(F_SCOL), scl(w, scl(1.0 - mirror, lacc))));
+            if (mirror > 0.0 && depth < P.max_depth) {
+              ST(F_W, w * mirror);
+              depth++;
+              const D3 d = d3(-hview.x, -hview.y, -hview.z);
+              const double s2 = 2.0 * dot(hn, d);
+              const D3 v = sub(d, scl(s2, hn));
+              c_refl++;
+              emit_ray(add(hp, scl(1e-4, v)), v, DBL_MAX);
+              state = ST_CLOSEST;
+            } else {
+              finish = true;
+            }
           }
         }
       }
@@ -704,14 +795,82 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
             float* out = reinterpret_cast<float*>(P.out) + o;
             out[0] = (float)r; out[1] = (float)g; out[2] = (float)b;
           }
-          state = ST_FETCH;
+          state = heads_left > 0 ? ST_FETCH : ST_DONE;
         }
       }
     }
     asm volatile("" ::: "memory");
+
+    // ---- lend idle lanes to owners' extra rays (extra lights in order, then reflection) ----
+    {
+      const bool idle = (state == ST_FETCH || state == ST_DONE);
+      const unsigned long long I = __ballot(idle);
+      if (I != 0ull && __ballot(want > 0) != 0ull) {
+        if (idle) ltask[threadIdx.x] = kTaskNone;
+        int incl = want;   // inclusive prefix sum of want over the wave
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const int v = __shfl_up(incl, o);
+          if (lane >= o) incl += v;
+        }
+        wave_lds_sync();
+        const int off = incl - want;
+        const int avail = (int)__popcll(I);   // __popcll is unsigned: keep the subtraction signed
+        const int got = min(want, max(0, avail - off));
+        if (got > 0) {
+          const D3 hp = LD3(F_HP);
+          const int n_extra_lights = P.n_lights - light - 1;
+          for (int t = 0; t < got; ++t) {
+            const int ht = wbase + kth_set_bit(I, off + t);
+            D3 o, d;
+            double tl;
+            uint32_t tw;
+            if (t < n_extra_lights) {
+              const int j = light + 1 + t;
+              const double* L6 = P.lights + 6 * j;
+              const D3 to_l = sub(d3(L6[0], L6[1], L6[2]), hp);
+              const D3 l = normalize(to_l);
+              o = add(hp, scl(1e-4, l));
+              d = normalize(l);
+              tl = sqrt(dot(to_l, to_l));
+              tw = (uint32_t)lane | ((uint32_t)j << 8);
+              c_shadow++;
+            } else {   // reflection ray (same formula as the owner's own emission)
+              const D3 hn = LD3(F_HN), hv = LD3(F_HVIEW);
+              const D3 dd = d3(-hv.x, -hv.y, -hv.z);
+              const double s2 = 2.0 * dot(hn, dd);
+              const D3 v = sub(dd, scl(s2, hn));
+              o = add(hp, scl(1e-4, v));
+              d = normalize(v);
+              tl = DBL_MAX;
+              tw = (uint32_t)lane | kTaskRefl;
+              c_refl++;
+              refl_h = ht - wbase;
+            }
+            lds_d[0 * kBlock + ht] = o.x; lds_d[1 * kBlock + ht] = o.y; lds_d[2 * kBlock + ht] = o.z;
+            lds_d[3 * kBlock + ht] = d.x; lds_d[4 * kBlock + ht] = d.y; lds_d[5 * kBlock + ht] = d.z;
+            lds_d[6 * kBlock + ht] = tl;
+            ltask[ht] = tw;
+          }
+          batch_end = light + 1 + min(got, n_extra_lights);
+        }
+        wave_lds_sync();
+        if (idle) {
+          htask = ltask[threadIdx.x];
+          if (htask != kTaskNone) state = (htask & kTaskRefl) ? ST_HCLOSEST : ST_HSHADOW;
+        }
+      }
+    }
     if (STATS) { const unsigned long long t = stamp(); d_shade += t - t_stamp; t_stamp = t; }
   }
 
+  if (STATS && lane == 0) {
+    unsigned long long* wl = P.wavelog + 4 * ((size_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6));
+    wl[0] = w_start;
+    wl[1] = w_refill;
+    wl[2] = __builtin_amdgcn_s_memrealtime();
+    wl[3] = w_pixels;
+  }
   // ---------------- counters: one atomic per wave and counter ----------------
   const unsigned long long s0 = wave_sum(c_primary), s1 = wave_sum(c_shadow), s2 = wave_sum(c_refl);
   unsigned long long s3 = 0, s4 = 0, s5 = 0;
@@ -794,9 +953,11 @@ const Variant kVariants[] = {
 };
 constexpr int kNumVariants = 3;
 constexpr int kMaxDepth = 4096;  // traversal stack entries (LDS ring + global spill)
-// LDS per block: 7 doubles of ray slot + min(stack_words, kShortStack) u32 per thread.
+// LDS per block: 7 doubles of ray slot, task + visibility words and
+// min(stack_words, kShortStack) stack entries per thread.
 size_t lds_bytes(int stack_words) {
-  return (size_t)kBlock * (7 * sizeof(double) + (size_t)std::min(stack_words, kShortStack) * sizeof(uint32_t));
+  return (size_t)kBlock *
+         (7 * sizeof(double) + (2 + (size_t)std::min(stack_words, kShortStack)) * sizeof(uint32_t));
 }
 
 }  // namespace
@@ -821,6 +982,7 @@ struct rt_scene {
   int stack_words = 1;          // LDS stack entries per thread (>= tree depth)
   double* d_pstate = nullptr;   // [kFields][nslots]
   uint32_t* d_spill = nullptr;  // [stack_words][nslots] (only when stack_words > kShortStack)
+  unsigned long long* d_wavelog = nullptr;   // [nslots / 64][4]
   size_t nslots = 0;
   double* d_lights = nullptr;   // [RT_MAX_LIGHTS][6]
   int cached_lights = -1;       // light count currently in d_lights
@@ -1245,6 +1407,11 @@ int rt_scene_upload(const rt_scene_soa* s, const rt_bvh_soa* b, int device, rt_s
     return fail(RT_ERR_HIP, "hipMalloc of path state failed");
   }
   sc->bytes += (long long)(sc->nslots * kFields * sizeof(double) + RT_MAX_LIGHTS * 6 * sizeof(double));
+  if (hipMalloc(reinterpret_cast<void**>(&sc->d_wavelog), sc->nslots / 64 * 4 * sizeof(unsigned long long)) !=
+      hipSuccess) {
+    rt_scene_free(sc);
+    return fail(RT_ERR_HIP, "hipMalloc of wave log failed");
+  }
   if (sc->stack_words > kShortStack) {
     const size_t sb = sc->nslots * (size_t)sc->stack_words * sizeof(uint32_t);
     if (hipMalloc(reinterpret_cast<void**>(&sc->d_spill), sb) != hipSuccess) {
@@ -1326,6 +1493,7 @@ int rt_launch_compute_image(rt_scene* sc, const rt_render_params* p, void* d_out
   P.lights = sc->d_lights;
   P.pstate = sc->d_pstate;
   P.spill = sc->d_spill;
+  P.wavelog = sc->d_wavelog;
   P.nslots = sc->nslots;
   P.spp_n = p->spp_n;
   P.row_begin = scount == 1 ? std::max(0, p->row_begin) : 0;
@@ -1396,6 +1564,15 @@ int rt_debug_counters(rt_scene* sc, unsigned long long* out, int n) {
   return std::min(n, kCtrWords);
 }
 
+long long rt_debug_wave_log(rt_scene* sc, unsigned long long* out, long long n) {
+  if (!sc || !out || n <= 0) return fail(RT_ERR_INVALID, "rt_debug_wave_log: bad argument");
+  HIP_TRY(hipSetDevice(sc->device));
+  HIP_TRY(hipDeviceSynchronize());
+  const long long words = std::min<long long>(n, (long long)(sc->nslots / 64 * 4));
+  HIP_TRY(hipMemcpy(out, sc->d_wavelog, (size_t)words * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  return words;
+}
+
 int rt_last_kernel_ms(rt_scene* sc, float* ms) {
   if (!sc || !ms || !sc->timed) return fail(RT_ERR_INVALID, "rt_last_kernel_ms: no launch recorded");
   HIP_TRY(hipEventSynchronize(sc->ev1));
@@ -1408,7 +1585,7 @@ void rt_scene_free(rt_scene* sc) {
   (void)hipSetDevice(sc->device);
   void* ptrs[] = {sc->d_nodes, sc->d_nodes4, sc->d_tris, sc->d_shade, sc->d_fnorm, sc->d_vnorm, sc->d_tu,
                   sc->d_tv, sc->d_texels, sc->d_mats, sc->d_ctr, sc->d_pstate, sc->d_lights, sc->d_spill,
-                  sc->d_slot2dev};
+                  sc->d_slot2dev, sc->d_wavelog};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   if (sc->ev0) (void)hipEventDestroy(sc->ev0);

@@ -225,6 +225,14 @@ class DeviceScene:
                  26: "stack_spills", 27: "node_lines", 28: "leaf_lines", 29: "big_leaf_tests"}
         return {v: int(buf[k]) for k, v in names.items()}
 
+    def wave_log(self, max_waves=1 << 16):
+        """Per-wave {start, last fetch, end, pixels} of the last STATS launch (rt_debug_wave_log)."""
+        buf = np.zeros(4 * max_waves, dtype=np.uint64)
+        n = hip_lib().rt_debug_wave_log(self._h, buf.ctypes.data_as(C.POINTER(C.c_ulonglong)), len(buf))
+        if n < 0:
+            _check_hip(int(n), "rt_debug_wave_log")
+        return buf[:n].reshape(-1, 4)
+
     def last_kernel_ms(self):
         ms = C.c_float(0.0)
         _check_hip(hip_lib().rt_last_kernel_ms(self._h, C.byref(ms)), "rt_last_kernel_ms")
