@@ -98,8 +98,9 @@ enum : int { CS_PRIMARY = 8, CS_SHADOW, CS_REFLECT, CS_NODES, CS_TRIS, CS_HITS, 
 enum : int {
   CD_NODE_ITERS = 16, CD_NODE_LANES, CD_LEAF_ITERS, CD_LEAF_LANES, CD_TRAV_CYCLES, CD_SHADE_CYCLES,
   CD_FETCH_CYCLES, CD_OUTER_ITERS, CD_TRAV_ROUNDS, CD_TRAV_ROUND_LANES, CD_SPILLS, CD_NODE_LINES,
-  CD_LEAF_LINES, CD_BIG_LEAF_TESTS
+  CD_LEAF_LINES, CD_BIG_LEAF_TESTS, CD_GUARD = 31   // CD_GUARD: a wave hit the iteration guard
 };
+constexpr unsigned kGuardIters = 1u << 24;   // persistent-loop watchdog (never reached by a correct kernel)
 
 struct KParams {
   const GNode* nodes;
@@ -275,6 +276,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
   uint32_t* ltask = reinterpret_cast<uint32_t*>(lds_raw + 7 * kBlock * sizeof(double));   // [kBlock]
   uint32_t* lvis = ltask + kBlock;                                                             // [kBlock]
   uint32_t* stk = lvis + kBlock + threadIdx.x;
+  lvis[threadIdx.x] = 0u;
   const int wbase = threadIdx.x & ~63;   // first thread of this wave
   uint32_t* spill = P.spill + (size_t)blockIdx.x * kBlock + threadIdx.x;
 
@@ -336,7 +338,12 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
     state = ST_CLOSEST;
   };
 
+  unsigned guard = 0;
   for (;;) {
+    if (++guard > kGuardIters) {   // watchdog: end the wave instead of spinning, flag the launch
+      if (lane == 0) atomicOr(&P.ctr[CD_GUARD], 1ull);
+      break;
+    }
     if (STATS) { d_outer++; t_stamp = stamp(); }
     // ---------------- refill idle lanes (one atomic per wave) ----------------
     unsigned long long m_fetch = __ballot(state == ST_FETCH);
@@ -1532,6 +1539,8 @@ int rt_launch_compute_image(rt_scene* sc, const rt_render_params* p, void* d_out
     stats->tri_tests = (long long)c[CS_TRIS];
     stats->closest_hits = (long long)c[CS_HITS];
     stats->pixels = (long long)c[CS_PIXELS];
+    if (c[CD_GUARD] != 0)
+      return fail(RT_ERR_HIP, "rt_launch_compute_image: persistent-loop watchdog fired (kernel bug)");
   }
   return RT_OK;
 }

@@ -11,8 +11,10 @@
 #define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 
 template <int LOADS>
-__global__ void __launch_bounds__(256) chase(const uint4* __restrict__ tab, int nrec, int iters, int group, unsigned* out) {
+__global__ void __launch_bounds__(256) chase(const uint4* __restrict__ tab, int nrec, int iters, int group, unsigned* out,
+                                             int active) {
   const int lane = threadIdx.x & 63;
+  if (lane >= active) return;   // partially active waves: does the gather cost scale with lanes?
   // lanes in the same group of `group` lanes start on the same record
   unsigned idx = (unsigned)(((lane / group) * 7919u + blockIdx.x * 131u + (threadIdx.x >> 6) * 17u) % (unsigned)nrec);
   unsigned acc = 0;
@@ -32,12 +34,12 @@ __global__ void __launch_bounds__(256) chase(const uint4* __restrict__ tab, int 
 }
 
 template <int LOADS>
-float run(const uint4* d_tab, int nrec, int iters, int group, unsigned* d_out, int blocks) {
+float run(const uint4* d_tab, int nrec, int iters, int group, unsigned* d_out, int blocks, int active = 64) {
   hipEvent_t a, b;
   CHECK(hipEventCreate(&a)); CHECK(hipEventCreate(&b));
-  chase<LOADS><<<blocks, 256>>>(d_tab, nrec, 10, group, d_out);
+  chase<LOADS><<<blocks, 256>>>(d_tab, nrec, 10, group, d_out, active);
   CHECK(hipEventRecord(a));
-  chase<LOADS><<<blocks, 256>>>(d_tab, nrec, iters, group, d_out);
+  chase<LOADS><<<blocks, 256>>>(d_tab, nrec, iters, group, d_out, active);
   CHECK(hipEventRecord(b));
   CHECK(hipEventSynchronize(b));
   float ms; CHECK(hipEventElapsedTime(&ms, a, b));
@@ -74,6 +76,12 @@ int main() {
         printf("  %d loads: %6.1f cyc/visit/CU (%5.1f per load)", L[i], cyc, cyc / L[i]);
       }
       printf("\n");
+    }
+    for (int active : {64, 32, 16, 4}) {
+      const float ms = run<7>(d_tab, nrec, iters, 1, d_out, blocks, active);
+      const float ms2 = run<7>(d_tab, nrec, iters, 64, d_out, blocks, active);
+      const double c1 = ms * 1e-3 * ghz * 1e9 / ((double)iters * 16), c2 = ms2 * 1e-3 * ghz * 1e9 / ((double)iters * 16);
+      printf("records %3d active lanes %2d, 7 loads: divergent %6.1f cyc/visit/CU, coherent %6.1f\n", nrec, active, c1, c2);
     }
     CHECK(hipFree(d_tab)); CHECK(hipFree(d_out));
   }
