@@ -969,6 +969,20 @@ size_t lds_bytes(int stack_words) {
 
 }  // namespace
 
+// Per-launch mutable state.  A scene owns a ring of kContexts so launches on
+// different streams can run concurrently: the drain of one frame (waves finishing
+// their last pixels) overlaps the next frame's work.  A context is
+// reused only after its previous launch completed (stream wait on `done`).
+constexpr int kContexts = 4;
+struct LaunchCtx {
+  unsigned long long* d_ctr = nullptr;       // [kCtrWords] work heads, stats, diagnostics
+  double* d_pstate = nullptr;                // [nslots][kFields] path state
+  uint32_t* d_spill = nullptr;               // [stack_words][nslots] (only when stack_words > kShortStack)
+  unsigned long long* d_wavelog = nullptr;   // [nslots / 64][4]
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;   // kernel start / end (timing, reuse fence)
+  bool used = false;
+};
+
 struct rt_scene {
   int device = 0;
   GNode* d_nodes = nullptr;
@@ -981,15 +995,14 @@ struct rt_scene {
   double* d_tv = nullptr;
   unsigned char* d_texels = nullptr;
   GMat* d_mats = nullptr;
-  unsigned long long* d_ctr = nullptr;
   int n_gnodes = 0;
   long long n_tris = 0;
   int n_meshes = 0;
   int depth = 0;
   int stack_words = 1;          // LDS stack entries per thread (>= tree depth)
-  double* d_pstate = nullptr;   // [kFields][nslots]
-  uint32_t* d_spill = nullptr;  // [stack_words][nslots] (only when stack_words > kShortStack)
-  unsigned long long* d_wavelog = nullptr;   // [nslots / 64][4]
+  LaunchCtx ctx[kContexts];
+  int next_ctx = 0;             // ring cursor
+  int last_ctx = -1;            // context of the most recent launch
   size_t nslots = 0;
   double* d_lights = nullptr;   // [RT_MAX_LIGHTS][6]
   int cached_lights = -1;       // light count currently in d_lights
@@ -1001,8 +1014,6 @@ struct rt_scene {
   int blocks_per_cu[kNumVariants] = {0, 0, 0};
   GNode4* d_nodes4 = nullptr;
   int n_gnodes4 = 0;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  bool timed = false;
 };
 
 namespace {
@@ -1373,10 +1384,6 @@ int rt_scene_upload(const rt_scene_soa* s, const rt_bvh_soa* b, int device, rt_s
   if (rc == RT_OK) rc = upload(&sc->d_tv, tv, bytes);
   if (rc == RT_OK) rc = upload(&sc->d_texels, texels, bytes);
   if (rc == RT_OK) rc = upload(&sc->d_mats, mats, bytes);
-  if (rc == RT_OK) {
-    std::vector<unsigned long long> z(kCtrWords, 0);
-    rc = upload(&sc->d_ctr, z, bytes);
-  }
   if (rc != RT_OK) {
     rt_scene_free(sc);
     return rc;
@@ -1408,28 +1415,25 @@ int rt_scene_upload(const rt_scene_soa* s, const rt_bvh_soa* b, int device, rt_s
     max_blocks = std::max(max_blocks, nb);
   }
   sc->nslots = (size_t)sc->n_cu * max_blocks * kBlock;
-  if (hipMalloc(reinterpret_cast<void**>(&sc->d_pstate), sc->nslots * kFields * sizeof(double)) != hipSuccess ||
-      hipMalloc(reinterpret_cast<void**>(&sc->d_lights), RT_MAX_LIGHTS * 6 * sizeof(double)) != hipSuccess) {
+  if (hipMalloc(reinterpret_cast<void**>(&sc->d_lights), RT_MAX_LIGHTS * 6 * sizeof(double)) != hipSuccess) {
     rt_scene_free(sc);
-    return fail(RT_ERR_HIP, "hipMalloc of path state failed");
+    return fail(RT_ERR_HIP, "hipMalloc of lights failed");
   }
-  sc->bytes += (long long)(sc->nslots * kFields * sizeof(double) + RT_MAX_LIGHTS * 6 * sizeof(double));
-  if (hipMalloc(reinterpret_cast<void**>(&sc->d_wavelog), sc->nslots / 64 * 4 * sizeof(unsigned long long)) !=
-      hipSuccess) {
-    rt_scene_free(sc);
-    return fail(RT_ERR_HIP, "hipMalloc of wave log failed");
-  }
-  if (sc->stack_words > kShortStack) {
-    const size_t sb = sc->nslots * (size_t)sc->stack_words * sizeof(uint32_t);
-    if (hipMalloc(reinterpret_cast<void**>(&sc->d_spill), sb) != hipSuccess) {
+  sc->bytes += (long long)(RT_MAX_LIGHTS * 6 * sizeof(double));
+  for (LaunchCtx& c : sc->ctx) {
+    const size_t pb = sc->nslots * kFields * sizeof(double);
+    const size_t wb = sc->nslots / 64 * 4 * sizeof(unsigned long long);
+    const size_t sb = sc->stack_words > kShortStack ? sc->nslots * (size_t)sc->stack_words * sizeof(uint32_t) : 0;
+    if (hipMalloc(reinterpret_cast<void**>(&c.d_ctr), kCtrWords * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&c.d_pstate), pb) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&c.d_wavelog), wb) != hipSuccess ||
+        (sb > 0 && hipMalloc(reinterpret_cast<void**>(&c.d_spill), sb) != hipSuccess) ||
+        hipMemset(c.d_ctr, 0, kCtrWords * sizeof(unsigned long long)) != hipSuccess ||
+        hipEventCreate(&c.ev0) != hipSuccess || hipEventCreate(&c.ev1) != hipSuccess) {
       rt_scene_free(sc);
-      return fail(RT_ERR_HIP, "hipMalloc of traversal-stack spill failed");
+      return fail(RT_ERR_HIP, "allocation of launch contexts failed");
     }
-    sc->bytes += (long long)sb;
-  }
-  if (hipEventCreate(&sc->ev0) != hipSuccess || hipEventCreate(&sc->ev1) != hipSuccess) {
-    rt_scene_free(sc);
-    return fail(RT_ERR_HIP, "hipEventCreate failed");
+    sc->bytes += (long long)(kCtrWords * sizeof(unsigned long long) + pb + wb + sb);
   }
   *out = sc;
   return RT_OK;
@@ -1472,7 +1476,9 @@ int rt_launch_compute_image(rt_scene* sc, const rt_render_params* p, void* d_out
   std::memset(&P, 0, sizeof P);
   P.nodes = sc->d_nodes; P.nodes4 = sc->d_nodes4; P.tris = sc->d_tris; P.slot2dev = sc->d_slot2dev; P.shade = sc->d_shade; P.fnorm = sc->d_fnorm;
   P.vnorm = sc->d_vnorm; P.tu = sc->d_tu; P.tv = sc->d_tv; P.texels = sc->d_texels; P.mats = sc->d_mats;
-  P.ctr = sc->d_ctr;
+  LaunchCtx& C = sc->ctx[sc->next_ctx];
+  const int ci = sc->next_ctx;
+  P.ctr = C.d_ctr;
   P.out = d_out;
   P.n_gnodes = sc->n_gnodes;
   P.out_fmt = p->out_format;
@@ -1498,9 +1504,9 @@ int rt_launch_compute_image(rt_scene* sc, const rt_render_params* p, void* d_out
     }
   }
   P.lights = sc->d_lights;
-  P.pstate = sc->d_pstate;
-  P.spill = sc->d_spill;
-  P.wavelog = sc->d_wavelog;
+  P.pstate = C.d_pstate;
+  P.spill = C.d_spill;
+  P.wavelog = C.d_wavelog;
   P.nslots = sc->nslots;
   P.spp_n = p->spp_n;
   P.row_begin = scount == 1 ? std::max(0, p->row_begin) : 0;
@@ -1518,19 +1524,22 @@ int rt_launch_compute_image(rt_scene* sc, const rt_render_params* p, void* d_out
   blocks = std::max<long long>(1, std::min<long long>(blocks, (waves_needed + 3) / 4));
   blocks = std::min<long long>(blocks, (long long)(sc->nslots / kBlock));
 
-  HIP_TRY(hipMemsetAsync(sc->d_ctr, 0, kCtrWords * sizeof(unsigned long long), st));
-  HIP_TRY(hipEventRecord(sc->ev0, st));
+  if (C.used) HIP_TRY(hipStreamWaitEvent(st, C.ev1, 0));   // previous launch on this context done
+  HIP_TRY(hipMemsetAsync(C.d_ctr, 0, kCtrWords * sizeof(unsigned long long), st));
+  HIP_TRY(hipEventRecord(C.ev0, st));
   if (rows > 0) {
     void* args[] = {&P};
     HIP_TRY(hipLaunchKernel(reinterpret_cast<const void*>(kVariants[v].fn), dim3((unsigned)blocks), dim3(kBlock),
                             args, lds, st));
   }
-  HIP_TRY(hipEventRecord(sc->ev1, st));
-  sc->timed = true;
+  HIP_TRY(hipEventRecord(C.ev1, st));
+  C.used = true;
+  sc->last_ctx = ci;
+  sc->next_ctx = (ci + 1) % kContexts;
   if (stats) {
     HIP_TRY(hipStreamSynchronize(st));
     unsigned long long c[kCtrWords];
-    HIP_TRY(hipMemcpy(c, sc->d_ctr, sizeof c, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(c, C.d_ctr, sizeof c, hipMemcpyDeviceToHost));
     std::memset(stats, 0, sizeof *stats);
     stats->primary_rays = (long long)c[CS_PRIMARY];
     stats->shadow_rays = (long long)c[CS_SHADOW];
@@ -1568,7 +1577,8 @@ int rt_debug_counters(rt_scene* sc, unsigned long long* out, int n) {
   HIP_TRY(hipSetDevice(sc->device));
   HIP_TRY(hipDeviceSynchronize());
   unsigned long long c[kCtrWords];
-  HIP_TRY(hipMemcpy(c, sc->d_ctr, sizeof c, hipMemcpyDeviceToHost));
+  if (sc->last_ctx < 0) return fail(RT_ERR_INVALID, "rt_debug_counters: no launch recorded");
+  HIP_TRY(hipMemcpy(c, sc->ctx[sc->last_ctx].d_ctr, sizeof c, hipMemcpyDeviceToHost));
   for (int i = 0; i < n && i < kCtrWords; ++i) out[i] = c[i];
   return std::min(n, kCtrWords);
 }
@@ -1578,27 +1588,35 @@ long long rt_debug_wave_log(rt_scene* sc, unsigned long long* out, long long n) 
   HIP_TRY(hipSetDevice(sc->device));
   HIP_TRY(hipDeviceSynchronize());
   const long long words = std::min<long long>(n, (long long)(sc->nslots / 64 * 4));
-  HIP_TRY(hipMemcpy(out, sc->d_wavelog, (size_t)words * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  if (sc->last_ctx < 0) return fail(RT_ERR_INVALID, "rt_debug_wave_log: no launch recorded");
+  HIP_TRY(hipMemcpy(out, sc->ctx[sc->last_ctx].d_wavelog, (size_t)words * sizeof(unsigned long long),
+                    hipMemcpyDeviceToHost));
   return words;
 }
 
 int rt_last_kernel_ms(rt_scene* sc, float* ms) {
-  if (!sc || !ms || !sc->timed) return fail(RT_ERR_INVALID, "rt_last_kernel_ms: no launch recorded");
-  HIP_TRY(hipEventSynchronize(sc->ev1));
-  HIP_TRY(hipEventElapsedTime(ms, sc->ev0, sc->ev1));
+  if (!sc || !ms || sc->last_ctx < 0) return fail(RT_ERR_INVALID, "rt_last_kernel_ms: no launch recorded");
+  const LaunchCtx& C = sc->ctx[sc->last_ctx];
+  HIP_TRY(hipEventSynchronize(C.ev1));
+  HIP_TRY(hipEventElapsedTime(ms, C.ev0, C.ev1));
   return RT_OK;
 }
 
 void rt_scene_free(rt_scene* sc) {
   if (!sc) return;
   (void)hipSetDevice(sc->device);
+  (void)hipDeviceSynchronize();   // launches may still be reading the scene
   void* ptrs[] = {sc->d_nodes, sc->d_nodes4, sc->d_tris, sc->d_shade, sc->d_fnorm, sc->d_vnorm, sc->d_tu,
-                  sc->d_tv, sc->d_texels, sc->d_mats, sc->d_ctr, sc->d_pstate, sc->d_lights, sc->d_spill,
-                  sc->d_slot2dev, sc->d_wavelog};
+                  sc->d_tv, sc->d_texels, sc->d_mats, sc->d_lights, sc->d_slot2dev};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
-  if (sc->ev0) (void)hipEventDestroy(sc->ev0);
-  if (sc->ev1) (void)hipEventDestroy(sc->ev1);
+  for (LaunchCtx& c : sc->ctx) {
+    void* cp[] = {c.d_ctr, c.d_pstate, c.d_spill, c.d_wavelog};
+    for (void* q : cp)
+      if (q) (void)hipFree(q);
+    if (c.ev0) (void)hipEventDestroy(c.ev0);
+    if (c.ev1) (void)hipEventDestroy(c.ev1);
+  }
   delete sc;
 }
 

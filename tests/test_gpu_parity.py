@@ -195,6 +195,33 @@ def test_deterministic_and_stream_launch():
     assert dev.last_kernel_ms() > 0
 
 
+def test_concurrent_launches_on_streams_are_independent():
+    # Frames in flight on several streams use separate launch contexts (path state,
+    # work heads): each result equals its serial render, bit for bit, also when more
+    # launches are issued than there are contexts (ring reuse waits on the old launch).
+    import torch
+
+    hs, dev, _ = Case.get("office")
+    jobs = []
+    for k in range(6):
+        p = hs.render_params(256, 144, 1)
+        p.out_format = rtamd.RT_OUT_RGB_F64
+        p.stripe_height, p.stripe_count, p.stripe_index = 8, 3, k % 3
+        if k == 5:
+            p.stripe_count, p.stripe_index = 1, 0
+        jobs.append(p)
+    serial = [dev.render(p)[0] for p in jobs]
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    bufs = [torch.zeros(s_.size, dtype=torch.float64, device="cuda") for s_ in serial]
+    for k, p in enumerate(jobs):
+        s = streams[k % 3]
+        with torch.cuda.stream(s):
+            dev.launch(p, bufs[k].data_ptr(), stats=False, stream=s.cuda_stream)
+    torch.cuda.synchronize()
+    for k in range(len(jobs)):
+        assert np.array_equal(bufs[k].cpu().numpy().reshape(serial[k].shape), serial[k]), k
+
+
 def test_full_size_office_1080p_parity():
     # BASELINE config 2 at full size: whole-frame fp64 parity and exact ray counts.
     hs, dev, orc = Case.get("office")
