@@ -59,6 +59,7 @@ def parse():
     ap.add_argument("--tris", type=int, default=0, help="random_tris triangle count")
     ap.add_argument("--cpu-row-stride", type=int, default=1, help="cpu_baseline renders every k-th row")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="cpu_baseline: minimum timed CPU work")
     ap.add_argument("--save", default="", help="rank 0: save the gathered image (.npy)")
     ap.add_argument("--streams", type=int, default=4, help="frames in flight (1 = strictly serial frames)")
     return ap.parse_args()
@@ -204,7 +205,8 @@ def main():
 
 
 def cpu_baseline(host, params, a):
-    """CPU oracle (reference CPU renderer restated in C, OpenMP) on every k-th row."""
+    """CPU oracle (reference CPU renderer restated in C, OpenMP): whole frames of the
+    same workload, repeated until --cpu-seconds of CPU work have been timed."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import pyoracle
 
@@ -215,10 +217,15 @@ def cpu_baseline(host, params, a):
     xs = np.arange(a.width)
     xy = np.stack(np.meshgrid(xs, ys), -1).reshape(-1, 2)
     p = host.render_params(a.width, a.height, a.spp)
+    rays, frames = 0, 0
     t0 = time.perf_counter()
-    _, cnt = orc.render_pixels(p, xy, pyoracle.MODE_REFERENCE, threads)
-    dt = time.perf_counter() - t0
-    rays = cnt.primary_rays + cnt.shadow_rays + cnt.reflection_rays
+    while True:
+        _, cnt = orc.render_pixels(p, xy, pyoracle.MODE_REFERENCE, threads)
+        rays += cnt.primary_rays + cnt.shadow_rays + cnt.reflection_rays
+        frames += 1
+        dt = time.perf_counter() - t0
+        if dt >= a.cpu_seconds:
+            break
     cpu_model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -232,9 +239,9 @@ def cpu_baseline(host, params, a):
         "unit": "Mrays/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"every {a.cpu_row_stride}th row of the same frame: {len(xy)} pixels, {rays} rays, "
+        "sample": f"{frames} x (every {a.cpu_row_stride}th row of the frame: {len(xy)} pixels), {rays} rays, "
                   f"{dt:.2f} s; reference-CPU-semantics oracle (recursive unordered fp64 BVH, "
-                  f"closest-hit shadows); extrapolated full-frame {dt * a.cpu_row_stride:.1f} s",
+                  f"closest-hit shadows, OpenMP over pixels)",
         "cpu_model": cpu_model,
         "nproc": os.cpu_count(),
         "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
