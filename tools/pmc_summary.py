@@ -43,10 +43,11 @@ def derive(c):
         d["hbm_write_bytes"] = g("WRITE_SIZE") * 1024
     if g("TCC_HIT_sum") and g("TCC_MISS_sum") is not None:
         d["l2_hit_rate"] = g("TCC_HIT_sum") / (g("TCC_HIT_sum") + g("TCC_MISS_sum"))
+    # GRBM_GUI_ACTIVE is summed over the 8 XCDs: per-XCD active cycles = GRBM / 8
     if g("TA_BUSY_avr") and g("GRBM_GUI_ACTIVE"):
-        d["ta_busy_frac"] = g("TA_BUSY_avr") / g("GRBM_GUI_ACTIVE")
+        d["ta_busy_frac"] = g("TA_BUSY_avr") / (g("GRBM_GUI_ACTIVE") / 8)
     if g("TD_TD_BUSY_sum") and g("GRBM_GUI_ACTIVE"):
-        d["td_busy_frac_per_instance_x256"] = g("TD_TD_BUSY_sum") / (256 * g("GRBM_GUI_ACTIVE"))
+        d["td_busy_frac"] = g("TD_TD_BUSY_sum") / 256 / (g("GRBM_GUI_ACTIVE") / 8)
     if g("TCP_TOTAL_CACHE_ACCESSES_sum") and g("TCP_TCC_READ_REQ_sum") is not None:
         d["l1_miss_to_l2_frac"] = g("TCP_TCC_READ_REQ_sum") / g("TCP_TOTAL_CACHE_ACCESSES_sum")
     return d
