@@ -82,6 +82,16 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// Raw buffer access (gfx9 resource word 3; no format conversion).
+constexpr int kBufWord3 = 0x00020000;
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ double buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+}
+__device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, double x) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, x), r, voff, soff, 0);
+}
+
 // Lane of the k-th (0-based) set bit of m (k < popcount(m)).
 __device__ __forceinline__ int kth_set_bit(unsigned long long m, int k) {
   int base = 0;
@@ -282,11 +292,16 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
 
   const int lane = threadIdx.x & 63;
   const unsigned long long lane_below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  double* ps = P.pstate + ((size_t)blockIdx.x * kBlock + threadIdx.x) * kFields;
-  auto LD = [&](int f) { return ps[f]; };
-  auto ST = [&](int f, double v) { ps[f] = v; };
-  auto LD3 = [&](int f) { return d3(ps[f], ps[f + 1], ps[f + 2]); };
-  auto ST3 = [&](int f, D3 v) { ps[f] = v.x; ps[f + 1] = v.y; ps[f + 2] = v.z; };
+  // path state, wave-interleaved [wave][field][64 lanes]: one field of a wave is 512
+  // contiguous bytes (4 lines per access instead of 64 with a per-lane record).
+  // Buffer ops: lane offset in one VGPR, field offset f*512 as an SGPR constant.
+  const __amdgpu_buffer_rsrc_t prs =
+      __builtin_amdgcn_make_buffer_rsrc(P.pstate, 0, (int)(P.nslots * kFields * sizeof(double)), kBufWord3);
+  const uint32_t pvo = ((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * (uint32_t)kFields * 64u + (uint32_t)lane) * 8u;
+  auto LD = [&](int f) { return buf_ld(prs, pvo, (uint32_t)f * 512u); };
+  auto ST = [&](int f, double v) { buf_st(prs, pvo, (uint32_t)f * 512u, v); };
+  auto LD3 = [&](int f) { return d3(LD(f), LD(f + 1), LD(f + 2)); };
+  auto ST3 = [&](int f, D3 v) { ST(f, v.x); ST(f + 1, v.y); ST(f + 2, v.z); };
 
   // wave-uniform work-head cursor
   int head = blockIdx.x % kGroups;
