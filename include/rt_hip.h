@@ -159,6 +159,19 @@ int rt_rows_in_shard(const rt_render_params* p);
 int rt_launch_compute_image(rt_scene* scene, const rt_render_params* p, void* d_out,
                             rt_stats* stats, void* stream);
 
+/* Adaptive supersampling pass: replaces adaptive_supersampling_device
+ * (mytracer_gpu.cu:162-229, launched at :83-109 with subp = 4, threshold = 0.02).
+ * d_primary: the primary pass of the SAME params rendered with
+ * RT_OUT_RGB_F64 (H x W x 3 doubles, device).  Every interior pixel whose
+ * squared colour differences to its 4 neighbours (x+1, y+1, x-1, y-1, in that
+ * order) sum above `threshold` is re-rendered with subp x subp stratified
+ * samples (averaged, clamped); all other pixels are copied from d_primary.
+ * d_out (H x W x 3, p->out_format) must not alias d_primary.  Full frame only
+ * (stripe_count 1, no row range).  stats (optional, synchronising) counts the
+ * rays of this pass; *n_selected (optional, synchronising) = re-rendered pixels. */
+int rt_launch_adaptive(rt_scene* scene, const rt_render_params* p, const double* d_primary, void* d_out, int subp,
+                       double threshold, rt_stats* stats, long long* n_selected, void* stream);
+
 /* Convenience for tests / CLI: renders into a HOST buffer (allocates a device
  * buffer internally, synchronous). */
 int rt_render_to_host(rt_scene* scene, const rt_render_params* p, void* host_out, rt_stats* stats);

@@ -145,6 +145,9 @@ struct KParams {
   int tiles_x;
   int pad1;
   long long n_tiles;
+  // list mode (adaptive pass): work items are full-frame pixel ids list[0 .. *list_count)
+  const uint32_t* list;
+  const unsigned long long* list_count;
 };
 
 // ---- fp64 vector ops (course vec4 semantics on xyz) ----
@@ -303,7 +306,9 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
   auto LD3 = [&](int f) { return d3(LD(f), LD(f + 1), LD(f + 2)); };
   auto ST3 = [&](int f, D3 v) { ST(f, v.x); ST(f + 1, v.y); ST(f + 2, v.z); };
 
-  // wave-uniform work-head cursor
+  // wave-uniform work-head cursor; in list mode the work count comes from the device
+  const long long n_list = P.list ? (long long)*P.list_count : 0;
+  const long long n_tiles = P.list ? (n_list + 63) / 64 : P.n_tiles;
   int head = blockIdx.x % kGroups;
   int heads_left = kGroups;
 
@@ -364,8 +369,8 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
     unsigned long long m_fetch = __ballot(state == ST_FETCH);
     unsigned long long m_busy = __ballot(state == ST_CLOSEST || state == ST_SHADOW || state >= ST_HSHADOW);
     while (m_fetch && (__popcll(m_fetch) >= kRefill || m_busy == 0) && heads_left > 0) {
-      const long long g0 = (P.n_tiles * head / kGroups) * 64;
-      const long long g1 = (P.n_tiles * (head + 1) / kGroups) * 64;
+      const long long g0 = (n_tiles * head / kGroups) * 64;
+      const long long g1 = (n_tiles * (head + 1) / kGroups) * 64;
       const int cnt = __popcll(m_fetch);
       const int leader = __ffsll((long long)m_fetch) - 1;
       unsigned long long base = 0;
@@ -381,12 +386,18 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
       if (state == ST_FETCH) {
         const long long wk = start + __popcll(m_fetch & lane_below);
         if (wk < g1) {
-          const long long tile = wk >> 6;
-          const int j = (int)(wk & 63);
-          const long long ty = tile / P.tiles_x;
-          const int tx = (int)(tile - ty * P.tiles_x);
-          px = tx * 8 + (j & 7);
-          lrow = (int)ty * 8 + (j >> 3);
+          if (P.list) {   // adaptive pass: pixel id from the compacted list (full frame)
+            const uint32_t id = wk < n_list ? P.list[wk] : 0xffffffffu;
+            px = id != 0xffffffffu ? (int)(id % (uint32_t)P.W) : P.W;
+            lrow = id != 0xffffffffu ? (int)(id / (uint32_t)P.W) : P.rows;
+          } else {
+            const long long tile = wk >> 6;
+            const int j = (int)(wk & 63);
+            const long long ty = tile / P.tiles_x;
+            const int tx = (int)(tile - ty * P.tiles_x);
+            px = tx * 8 + (j & 7);
+            lrow = (int)ty * 8 + (j >> 3);
+          }
           if (px < P.W && lrow < P.rows) {
             py = (P.stripe_count == 1)
                      ? P.row_begin + lrow
@@ -931,6 +942,60 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
   }
 }
 
+// ---------------------------------------------------------------------------
+// Adaptive supersampling, selection step (adaptive_supersampling_device,
+// mytracer_gpu.cu:162-200): an interior pixel is re-rendered with subp x subp
+// samples when the squared colour differences to its 4 neighbours in the
+// primary image sum above the threshold.  fp64, the reference's operation
+// order; one wave = one 8x8 tile, selected pixel ids are compacted with one
+// atomic per wave.  Pixels not selected are copied to the output here.
+__device__ __forceinline__ double nsq3(const double* a, const double* b) {
+  const double dx = a[0] - b[0], dy = a[1] - b[1], dz = a[2] - b[2];
+  return dx * dx + dy * dy + dz * dz;
+}
+
+__global__ void __launch_bounds__(256) adaptive_select_kernel(const double* prim, void* out, int out_fmt, int W,
+                                                              int H, double threshold, int tiles_x, long long n_tiles,
+                                                              uint32_t* list, unsigned long long* count) {
+  const long long tile = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int j = threadIdx.x & 63;
+  bool sel = false;
+  int x = 0, y = 0;
+  if (tile < n_tiles) {
+    const long long ty = tile / tiles_x;
+    x = (int)(tile - ty * tiles_x) * 8 + (j & 7);
+    y = (int)ty * 8 + (j >> 3);
+    if (x < W && y < H) {
+      const size_t o = 3 * ((size_t)y * W + x);
+      const double* c = prim + o;
+      if (x >= 1 && y >= 1 && x < W - 1 && y < H - 1) {
+        const double n = nsq3(c, c + 3) + nsq3(c, c + 3 * (size_t)W) + nsq3(c, c - 3) + nsq3(c, c - 3 * (size_t)W);
+        sel = n > threshold;
+      }
+      if (!sel) {
+        if (out_fmt == RT_OUT_RGB_F64) {
+          double* d = reinterpret_cast<double*>(out) + o;
+          d[0] = c[0]; d[1] = c[1]; d[2] = c[2];
+        } else {
+          float* d = reinterpret_cast<float*>(out) + o;
+          d[0] = (float)c[0]; d[1] = (float)c[1]; d[2] = (float)c[2];
+        }
+      }
+    }
+  }
+  const unsigned long long m = __ballot(sel);
+  if (m == 0ull) return;
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((long long)m) - 1;
+  unsigned long long base = 0;
+  if (lane == leader) base = atomicAdd(count, (unsigned long long)__popcll(m));
+  base = __shfl(base, leader);
+  if (sel) {
+    const unsigned long long below = lane == 0 ? 0ull : (m & (~0ull >> (64 - lane)));
+    list[base + __popcll(below)] = (uint32_t)((size_t)y * W + x);
+  }
+}
+
 // ===========================================================================
 // host side
 // ===========================================================================
@@ -1472,7 +1537,13 @@ int rt_rows_in_shard(const rt_render_params* p) {
   return rows;
 }
 
-int rt_launch_compute_image(rt_scene* sc, const rt_render_params* p, void* d_out, rt_stats* stats, void* stream) {
+}  // extern "C"
+
+namespace {
+// One render launch; list != nullptr: adaptive pass over the pixel ids list[0 .. *count)
+// (at most list_cap of them) of the full frame.
+int launch_render(rt_scene* sc, const rt_render_params* p, void* d_out, rt_stats* stats, void* stream,
+                  const uint32_t* list, const unsigned long long* count, long long list_cap) {
   if (!sc || !p || !d_out) return fail(RT_ERR_INVALID, "rt_launch_compute_image: null argument");
   if (p->camera.width <= 0 || p->camera.height <= 0) return fail(RT_ERR_INVALID, "bad image size");
   if (p->n_lights < 0 || p->n_lights > RT_MAX_LIGHTS) return fail(RT_ERR_INVALID, "n_lights out of range");
@@ -1530,7 +1601,9 @@ int rt_launch_compute_image(rt_scene* sc, const rt_render_params* p, void* d_out
   P.stripe_index = p->stripe_index;
   P.rows = rows;
   P.tiles_x = (P.W + 7) / 8;
-  P.n_tiles = (long long)P.tiles_x * ((rows + 7) / 8);
+  P.n_tiles = list ? (list_cap + 63) / 64 : (long long)P.tiles_x * ((rows + 7) / 8);
+  P.list = list;
+  P.list_count = count;
 
   const int v = (p->flags & RT_FLAG_TRAVERSAL_STATS) ? 2 : ((p->flags & RT_FLAG_WIDE_STATS) ? 1 : 0);
   const size_t lds = lds_bytes(sc->stack_words);
@@ -1568,6 +1641,54 @@ int rt_launch_compute_image(rt_scene* sc, const rt_render_params* p, void* d_out
   }
   return RT_OK;
 }
+}  // namespace
+
+extern "C" {
+
+int rt_launch_compute_image(rt_scene* sc, const rt_render_params* p, void* d_out, rt_stats* stats, void* stream) {
+  return launch_render(sc, p, d_out, stats, stream, nullptr, nullptr, 0);
+}
+
+int rt_launch_adaptive(rt_scene* sc, const rt_render_params* p, const double* d_primary, void* d_out, int subp,
+                       double threshold, rt_stats* stats, long long* n_selected, void* stream) {
+  if (!sc || !p || !d_primary || !d_out) return fail(RT_ERR_INVALID, "rt_launch_adaptive: null argument");
+  if (subp < 1 || subp > 64) return fail(RT_ERR_INVALID, "rt_launch_adaptive: subp must be in [1, 64]");
+  const int W = p->camera.width, H = p->camera.height;
+  if (W <= 0 || H <= 0) return fail(RT_ERR_INVALID, "bad image size");
+  if ((p->stripe_count > 1) || p->row_begin != 0 || (p->row_end > 0 && p->row_end != H))
+    return fail(RT_ERR_INVALID, "rt_launch_adaptive: needs the full frame (neighbour test), no stripes/row range");
+  if (p->out_format != RT_OUT_RGB_F32 && p->out_format != RT_OUT_RGB_F64) return fail(RT_ERR_INVALID, "bad out_format");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  HIP_TRY(hipSetDevice(sc->device));
+  const long long npix = (long long)W * H;
+  uint32_t* list = nullptr;
+  unsigned long long* cnt = nullptr;
+  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&list), (size_t)npix * sizeof(uint32_t), st));
+  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&cnt), sizeof(unsigned long long), st));
+  HIP_TRY(hipMemsetAsync(cnt, 0, sizeof(unsigned long long), st));
+  const int tiles_x = (W + 7) / 8;
+  const long long n_tiles = (long long)tiles_x * ((H + 7) / 8);
+  hipLaunchKernelGGL(adaptive_select_kernel, dim3((unsigned)((n_tiles + 3) / 4)), dim3(256), 0, st, d_primary, d_out,
+                     p->out_format, W, H, threshold, tiles_x, n_tiles, list, cnt);
+  HIP_TRY(hipGetLastError());
+  rt_render_params q = *p;
+  q.spp_n = subp;
+  q.stripe_count = 1;
+  q.stripe_index = 0;
+  q.row_begin = 0;
+  q.row_end = H;
+  int rc = launch_render(sc, &q, d_out, stats, stream, list, cnt, npix);
+  if (rc == RT_OK && n_selected) {
+    unsigned long long h = 0;
+    HIP_TRY(hipMemcpyAsync(&h, cnt, sizeof h, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    *n_selected = (long long)h;
+  }
+  (void)hipFreeAsync(list, st);
+  (void)hipFreeAsync(cnt, st);
+  return rc;
+}
+
 
 int rt_render_to_host(rt_scene* sc, const rt_render_params* p, void* host_out, rt_stats* stats) {
   if (!sc || !p || !host_out) return fail(RT_ERR_INVALID, "rt_render_to_host: null argument");

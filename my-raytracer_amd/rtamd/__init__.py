@@ -204,6 +204,32 @@ class DeviceScene:
                    "rt_launch_compute_image")
         return st
 
+    def launch_adaptive(self, params, d_primary, d_out, subp=4, threshold=0.02, stats=False, stream=None):
+        """Adaptive supersampling pass (rt_launch_adaptive) over device buffers (int pointers);
+        returns (Stats or None, number of re-rendered pixels)."""
+        st = abi.Stats() if stats else None
+        nsel = C.c_longlong(-1)
+        _check_hip(hip_lib().rt_launch_adaptive(self._h, C.byref(params), C.c_void_p(d_primary), C.c_void_p(d_out),
+                                                subp, threshold, C.byref(st) if st is not None else None,
+                                                C.byref(nsel), C.c_void_p(stream) if stream else None),
+                   "rt_launch_adaptive")
+        return st, int(nsel.value)
+
+    def render_adaptive(self, params, subp=4, threshold=0.02):
+        """Primary pass (fp64) + adaptive pass, the reference's launch_compute_image_device
+        (mytracer_gpu.cu:44-113); returns (image[H, W, 3], primary Stats, adaptive Stats, n_selected)."""
+        import torch
+
+        H, W = params.camera.height, params.camera.width
+        prim = torch.zeros((H, W, 3), dtype=torch.float64, device=f"cuda:{self.device}")
+        dtype = torch.float64 if params.out_format == RT_OUT_RGB_F64 else torch.float32
+        out = torch.zeros((H, W, 3), dtype=dtype, device=f"cuda:{self.device}")
+        q = abi.RenderParams.from_buffer_copy(params)
+        q.out_format = RT_OUT_RGB_F64
+        st0 = self.launch(q, prim.data_ptr(), stats=True)
+        st1, nsel = self.launch_adaptive(params, prim.data_ptr(), out.data_ptr(), subp, threshold, stats=True)
+        return out.cpu().numpy(), st0, st1, nsel
+
     def render(self, params):
         """Synchronous render to host; returns (image[rows, W, 3], Stats)."""
         rows = rows_in_shard(params)

@@ -157,6 +157,23 @@ class Oracle:
             raise RuntimeError("or_render_pixels failed")
         return out, cnt
 
+    def adaptive(self, params, primary, subp=4, threshold=0.02, mode=MODE_REFERENCE, threads=0):
+        """adaptive_supersampling_device (mytracer_gpu.cu:162-229) on the CPU: `primary` is the
+        fp64 primary image [H, W, 3] of `params` (1 ray per pixel).  Returns (image, Counts of the
+        supersampled rays, selection mask)."""
+        prim = np.ascontiguousarray(primary, dtype=np.float64)
+        H, W = prim.shape[:2]
+        sel = adaptive_selection(prim, threshold)
+        ys, xs = np.nonzero(sel)
+        img = prim.copy()
+        cnt = Counts()
+        if len(xs):
+            q = type(params).from_buffer_copy(params)
+            q.spp_n = subp
+            vals, cnt = self.render_pixels(q, np.stack([xs, ys], 1), mode, threads)
+            img[ys, xs] = vals
+        return img, cnt, sel
+
     def closest_hit(self, o, d, mode=MODE_REFERENCE):
         o = np.ascontiguousarray(o, dtype=np.float64)
         d = np.ascontiguousarray(d, dtype=np.float64)
@@ -197,3 +214,21 @@ def intersect_aabb(o, d, bmin, bmax):
 def median(values):
     a = np.ascontiguousarray(values, dtype=np.float64).copy()
     return float(lib().or_median(_dp(a), len(a)))
+
+
+def adaptive_selection(prim, threshold):
+    """Pixels adaptive_supersampling_device re-renders (mytracer_gpu.cu:183-198): interior pixels
+    whose squared colour distances to the neighbours (x+1, y+1, x-1, y-1) sum above threshold.
+    Same operation order as the reference: normSq = dx*dx + dy*dy + dz*dz, summed left to right."""
+    def nsq(a, b):
+        d = a - b
+        return (d[..., 0] * d[..., 0] + d[..., 1] * d[..., 1]) + d[..., 2] * d[..., 2]
+
+    H, W = prim.shape[:2]
+    sel = np.zeros((H, W), dtype=bool)
+    if H < 3 or W < 3:
+        return sel
+    c = prim[1:-1, 1:-1]
+    n = ((nsq(c, prim[1:-1, 2:]) + nsq(c, prim[2:, 1:-1])) + nsq(c, prim[1:-1, :-2])) + nsq(c, prim[:-2, 1:-1])
+    sel[1:-1, 1:-1] = n > threshold
+    return sel

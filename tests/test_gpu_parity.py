@@ -266,3 +266,39 @@ def test_cli_renders(tmp_path):
     assert r.returncode == 0, r.stderr
     assert out.read_bytes().startswith(b"P6\n64 48\n255\n")
     assert "Mrays/s" in r.stdout
+
+
+@pytest.mark.parametrize("kind,kw,w,h", [("office", {}, 192, 108), ("cornell", {}, 80, 60)])
+def test_adaptive_pass_matches_oracle(kind, kw, w, h):
+    # adaptive_supersampling_device (mytracer_gpu.cu:162-229), subp 4, threshold 0.02.
+    # Both sides start from the oracle's primary image, so the selection is identical input-for-input.
+    import torch
+
+    hs, dev, orc = Case.get(kind, **kw)
+    p = hs.render_params(w, h, 1)
+    prim, _ = orc.render(p)
+    ref, cnt, sel = orc.adaptive(p, prim, subp=4, threshold=0.02)
+    assert sel.sum() > 0
+    d_prim = torch.from_numpy(prim).cuda()
+    for fmt, tol in ((rtamd.RT_OUT_RGB_F64, TOL64), (rtamd.RT_OUT_RGB_F32, TOL32)):
+        p.out_format = fmt
+        out = torch.zeros((h, w, 3), dtype=torch.float64 if fmt == rtamd.RT_OUT_RGB_F64 else torch.float32,
+                          device="cuda")
+        st, nsel = dev.launch_adaptive(p, d_prim.data_ptr(), out.data_ptr(), 4, 0.02, stats=True)
+        assert nsel == int(sel.sum())
+        assert np.abs(out.cpu().numpy().astype(np.float64) - ref).max() <= tol
+        assert counts(st) == [cnt.primary_rays, cnt.shadow_rays, cnt.reflection_rays]
+
+
+def test_adaptive_end_to_end_and_full_frame_only():
+    hs, dev, orc = Case.get("office")
+    p = hs.render_params(128, 72, 1)
+    p.out_format = rtamd.RT_OUT_RGB_F64
+    img, st0, st1, nsel = dev.render_adaptive(p)
+    prim, _ = orc.render(p)
+    ref, cnt, sel = orc.adaptive(p, prim)
+    assert abs(nsel - int(sel.sum())) <= 2      # GPU primary within 1e-12 of the oracle's
+    assert np.abs(img - ref)[~sel].max() <= TOL64
+    p.stripe_count, p.stripe_height = 2, 16
+    with pytest.raises(rtamd.RtError):
+        dev.render_adaptive(p)
