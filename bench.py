@@ -62,6 +62,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="cpu_baseline: minimum timed CPU work")
     ap.add_argument("--save", default="", help="rank 0: save the gathered image (.npy)")
     ap.add_argument("--streams", type=int, default=4, help="frames in flight (1 = strictly serial frames)")
+    ap.add_argument("--adaptive", action="store_true",
+                    help="each frame = primary pass + adaptive supersampling pass (subp 4, threshold 0.02, "
+                         "mytracer_gpu.cu:83-109); single GPU")
     return ap.parse_args()
 
 
@@ -72,6 +75,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if a.gpus != world and world > 1:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE {world}")
+    if a.adaptive and world > 1:
+        raise SystemExit("--adaptive needs the full frame on one GPU (neighbour test)")
     n = world
     torch.cuda.set_device(local)
     if n > 1:
@@ -94,6 +99,7 @@ def main():
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(S - 1)]
     buf = bufs[0]
     stream = streams[0].cuda_stream
+    prims = [torch.zeros((a.height, W, 3), dtype=torch.float64, device="cuda") for _ in range(S)] if a.adaptive else []
 
     # ---- counters: canonical rays + algorithmic bytes (untimed launches) ----
     st = gpu.launch(params, buf.data_ptr(), stats=True, stream=stream)
@@ -101,6 +107,16 @@ def main():
     tst = gpu.launch(params, buf.data_ptr(), stats=True, stream=stream)
     params.flags = 0
     rays_local = st.primary_rays + st.shadow_rays + st.reflection_rays
+    adaptive_info = None
+    if a.adaptive:   # untimed: rays of the adaptive pass (selection depends on the primary image)
+        p64 = rtamd.abi.RenderParams.from_buffer_copy(params)
+        p64.out_format = rtamd.RT_OUT_RGB_F64
+        gpu.launch(p64, prims[0].data_ptr(), stats=True, stream=stream)
+        ast, nsel = gpu.launch_adaptive(params, prims[0].data_ptr(), buf.data_ptr(), 4, 0.02, stats=True,
+                                        stream=stream)
+        rays_local += ast.primary_rays + ast.shadow_rays + ast.reflection_rays
+        adaptive_info = {"pixels_supersampled": nsel, "subp": 4, "threshold": 0.02,
+                         "rays": ast.primary_rays + ast.shadow_rays + ast.reflection_rays}
     alg_bytes_local = 64 * tst.node_visits + 48 * tst.tri_tests + 64 * tst.closest_hits
 
     gather = StripeGather(a.height, W, STRIPE_H, n, rank, device="cuda")
@@ -116,7 +132,12 @@ def main():
             if timed:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(s)
-            gpu.launch(params, b.data_ptr(), stats=False, stream=s.cuda_stream)
+            if a.adaptive:
+                gpu.launch(p64, prims[k % S].data_ptr(), stats=False, stream=s.cuda_stream)
+                gpu.launch_adaptive(params, prims[k % S].data_ptr(), b.data_ptr(), 4, 0.02, stats=False,
+                                    stream=s.cuda_stream)
+            else:
+                gpu.launch(params, b.data_ptr(), stats=False, stream=s.cuda_stream)
             if timed:
                 e1.record(s)
                 starts.append(e0)
@@ -177,6 +198,7 @@ def main():
                                          "reflection": st.reflection_rays},
                 "parallelism": f"row-stripes x{n} (16-row interleave) + RCCL gather" if n > 1 else "single GPU",
                 "frames_in_flight": S,
+                "adaptive_pass": adaptive_info,
                 "host_bvh_build_s": round(build_s, 4),
                 "device_scene_MB": round(gpu.device_bytes / 1e6, 1),
             },

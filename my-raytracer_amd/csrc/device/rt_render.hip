@@ -145,9 +145,13 @@ struct KParams {
   int tiles_x;
   int pad1;
   long long n_tiles;
-  // list mode (adaptive pass): work items are full-frame pixel ids list[0 .. *list_count)
+  // list mode (adaptive pass): work item w = one sample (w % nsamp) of the full-frame pixel
+  // list[w / nsamp]; its trace() colour goes to sample_out[3w..3w+2] (summed in order later)
   const uint32_t* list;
   const unsigned long long* list_count;
+  double* sample_out;
+  int nsamp;
+  int pad2;
 };
 
 // ---- fp64 vector ops (course vec4 semantics on xyz) ----
@@ -307,14 +311,14 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
   auto ST3 = [&](int f, D3 v) { ST(f, v.x); ST(f + 1, v.y); ST(f + 2, v.z); };
 
   // wave-uniform work-head cursor; in list mode the work count comes from the device
-  const long long n_list = P.list ? (long long)*P.list_count : 0;
+  const long long n_list = P.list ? (long long)*P.list_count * P.nsamp : 0;   // work items
   const long long n_tiles = P.list ? (n_list + 63) / 64 : P.n_tiles;
   int head = blockIdx.x % kGroups;
   int heads_left = kGroups;
 
   // ---- per-lane state live across phases ----
   int state = ST_FETCH;
-  int px = 0, lrow = 0, py = 0, sample = 0, depth = 0, light = 0, mesh = 0;
+  int px = 0, lrow = 0, py = 0, sample = 0, depth = 0, light = 0, mesh = 0, item = 0;
   int best = kNoHit;        // device record of the closest hit
   int best_slot = kNoHit;   // its reference slot (tie-break key)
   double thit = DBL_MAX;
@@ -386,10 +390,11 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
       if (state == ST_FETCH) {
         const long long wk = start + __popcll(m_fetch & lane_below);
         if (wk < g1) {
-          if (P.list) {   // adaptive pass: pixel id from the compacted list (full frame)
-            const uint32_t id = wk < n_list ? P.list[wk] : 0xffffffffu;
+          if (P.list) {   // adaptive pass: one sample of a listed pixel (full frame)
+            const uint32_t id = wk < n_list ? P.list[wk / P.nsamp] : 0xffffffffu;
             px = id != 0xffffffffu ? (int)(id % (uint32_t)P.W) : P.W;
             lrow = id != 0xffffffffu ? (int)(id / (uint32_t)P.W) : P.rows;
+            item = (int)wk;
           } else {
             const long long tile = wk >> 6;
             const int j = (int)(wk & 63);
@@ -402,7 +407,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
             py = (P.stripe_count == 1)
                      ? P.row_begin + lrow
                      : ((lrow / P.stripe_h) * P.stripe_count + P.stripe_index) * P.stripe_h + (lrow % P.stripe_h);
-            sample = 0;
+            sample = P.list ? item % P.nsamp : 0;
             ST3(F_PCOL, d3(0, 0, 0));
             start_sample();
           }
@@ -811,7 +816,12 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
           }
         }
       }
-      if (finish) {
+      if (finish && P.list) {   // adaptive pass: this sample's trace() colour
+        const D3 c = LD3(F_SCOL);
+        double* so = P.sample_out + 3 * (size_t)item;
+        so[0] = c.x; so[1] = c.y; so[2] = c.z;
+        state = heads_left > 0 ? ST_FETCH : ST_DONE;
+      } else if (finish) {
         const D3 pcol = add(LD3(F_PCOL), LD3(F_SCOL));
         sample++;
         if (sample < P.spp_n * P.spp_n) {
@@ -993,6 +1003,34 @@ __global__ void __launch_bounds__(256) adaptive_select_kernel(const double* prim
   if (sel) {
     const unsigned long long below = lane == 0 ? 0ull : (m & (~0ull >> (64 - lane)));
     list[base + __popcll(below)] = (uint32_t)((size_t)y * W + x);
+  }
+}
+
+// Adaptive pass, final step (mytracer_gpu.cu:202-227): sum each listed pixel's
+// samples in (si, sj) order, divide by subp^2, clamp, store.
+__global__ void __launch_bounds__(256) adaptive_reduce_kernel(const uint32_t* list, const unsigned long long* count,
+                                                              const double* samples, int nsamp, void* out,
+                                                              int out_fmt) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)*count) return;
+  const double* s = samples + 3 * (size_t)i * nsamp;
+  double r = 0.0, g = 0.0, b = 0.0;
+  for (int k = 0; k < nsamp; ++k) {
+    r = r + s[3 * k];
+    g = g + s[3 * k + 1];
+    b = b + s[3 * k + 2];
+  }
+  const double nn = (double)nsamp;
+  r = stdmin(r / nn, 1.0);
+  g = stdmin(g / nn, 1.0);
+  b = stdmin(b / nn, 1.0);
+  const size_t o = 3 * (size_t)list[i];
+  if (out_fmt == RT_OUT_RGB_F64) {
+    double* d = reinterpret_cast<double*>(out) + o;
+    d[0] = r; d[1] = g; d[2] = b;
+  } else {
+    float* d = reinterpret_cast<float*>(out) + o;
+    d[0] = (float)r; d[1] = (float)g; d[2] = (float)b;
   }
 }
 
@@ -1543,7 +1581,8 @@ namespace {
 // One render launch; list != nullptr: adaptive pass over the pixel ids list[0 .. *count)
 // (at most list_cap of them) of the full frame.
 int launch_render(rt_scene* sc, const rt_render_params* p, void* d_out, rt_stats* stats, void* stream,
-                  const uint32_t* list, const unsigned long long* count, long long list_cap) {
+                  const uint32_t* list, const unsigned long long* count, long long list_cap,
+                  double* sample_out = nullptr) {
   if (!sc || !p || !d_out) return fail(RT_ERR_INVALID, "rt_launch_compute_image: null argument");
   if (p->camera.width <= 0 || p->camera.height <= 0) return fail(RT_ERR_INVALID, "bad image size");
   if (p->n_lights < 0 || p->n_lights > RT_MAX_LIGHTS) return fail(RT_ERR_INVALID, "n_lights out of range");
@@ -1601,9 +1640,11 @@ int launch_render(rt_scene* sc, const rt_render_params* p, void* d_out, rt_stats
   P.stripe_index = p->stripe_index;
   P.rows = rows;
   P.tiles_x = (P.W + 7) / 8;
-  P.n_tiles = list ? (list_cap + 63) / 64 : (long long)P.tiles_x * ((rows + 7) / 8);
+  P.nsamp = p->spp_n * p->spp_n;
+  P.n_tiles = list ? (list_cap * P.nsamp + 63) / 64 : (long long)P.tiles_x * ((rows + 7) / 8);
   P.list = list;
   P.list_count = count;
+  P.sample_out = sample_out;
 
   const int v = (p->flags & RT_FLAG_TRAVERSAL_STATS) ? 2 : ((p->flags & RT_FLAG_WIDE_STATS) ? 1 : 0);
   const size_t lds = lds_bytes(sc->stack_words);
@@ -1660,11 +1701,16 @@ int rt_launch_adaptive(rt_scene* sc, const rt_render_params* p, const double* d_
   if (p->out_format != RT_OUT_RGB_F32 && p->out_format != RT_OUT_RGB_F64) return fail(RT_ERR_INVALID, "bad out_format");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   HIP_TRY(hipSetDevice(sc->device));
-  const long long npix = (long long)W * H;
   uint32_t* list = nullptr;
   unsigned long long* cnt = nullptr;
-  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&list), (size_t)npix * sizeof(uint32_t), st));
+  double* samples = nullptr;
+  // interior pixels only can be selected
+  const long long cap = (long long)std::max(0, W - 2) * std::max(0, H - 2);
+  const int nsamp = subp * subp;
+  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&list), (size_t)std::max(1LL, cap) * sizeof(uint32_t), st));
   HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&cnt), sizeof(unsigned long long), st));
+  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&samples), (size_t)std::max(1LL, cap) * nsamp * 3 * sizeof(double),
+                         st));
   HIP_TRY(hipMemsetAsync(cnt, 0, sizeof(unsigned long long), st));
   const int tiles_x = (W + 7) / 8;
   const long long n_tiles = (long long)tiles_x * ((H + 7) / 8);
@@ -1677,7 +1723,12 @@ int rt_launch_adaptive(rt_scene* sc, const rt_render_params* p, const double* d_
   q.stripe_index = 0;
   q.row_begin = 0;
   q.row_end = H;
-  int rc = launch_render(sc, &q, d_out, stats, stream, list, cnt, npix);
+  int rc = launch_render(sc, &q, d_out, stats, stream, list, cnt, cap, samples);
+  if (rc == RT_OK && cap > 0) {
+    hipLaunchKernelGGL(adaptive_reduce_kernel, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, st, list, cnt,
+                       samples, nsamp, d_out, p->out_format);
+    HIP_TRY(hipGetLastError());
+  }
   if (rc == RT_OK && n_selected) {
     unsigned long long h = 0;
     HIP_TRY(hipMemcpyAsync(&h, cnt, sizeof h, hipMemcpyDeviceToHost, st));
@@ -1686,6 +1737,7 @@ int rt_launch_adaptive(rt_scene* sc, const rt_render_params* p, const double* d_
   }
   (void)hipFreeAsync(list, st);
   (void)hipFreeAsync(cnt, st);
+  (void)hipFreeAsync(samples, st);
   return rc;
 }
 

@@ -208,10 +208,11 @@ class DeviceScene:
         """Adaptive supersampling pass (rt_launch_adaptive) over device buffers (int pointers);
         returns (Stats or None, number of re-rendered pixels)."""
         st = abi.Stats() if stats else None
-        nsel = C.c_longlong(-1)
+        nsel = C.c_longlong(-1)   # only requested with stats (reading it synchronises)
         _check_hip(hip_lib().rt_launch_adaptive(self._h, C.byref(params), C.c_void_p(d_primary), C.c_void_p(d_out),
                                                 subp, threshold, C.byref(st) if st is not None else None,
-                                                C.byref(nsel), C.c_void_p(stream) if stream else None),
+                                                C.byref(nsel) if stats else None,
+                                                C.c_void_p(stream) if stream else None),
                    "rt_launch_adaptive")
         return st, int(nsel.value)
 
