@@ -17,6 +17,8 @@
 #include <cstdio>
 #include <cstring>
 #include <stdexcept>
+#include <thread>
+#include <cstdlib>
 
 namespace rt {
 
@@ -203,61 +205,53 @@ void build_data(const HostScene& scene, SoA& s) {
 // order, so children get the same ids (nodesUsed_ at split time, :456-458).
 // Triangle centroids ((v0+v1+v2)/3.0, :492/:535) are cached per slot and
 // swapped with the slot's data, which leaves every value bit-identical.
-void build_bvh_soa(SoA& s, BvhSoA& b) {
-  b = BvhSoA();
-  const long long N = s.n_vertex_idx / 3;
-  if (N <= 0) return;
-  const size_t cap = 2 * (size_t)N - 1;
-  b.bb_min.assign(3 * cap, 0.0);
-  b.bb_max.assign(3 * cap, 0.0);
-  b.left_child.assign(cap, 0);
-  b.first_tri.assign(cap, 0);
-  b.tri_count.assign(cap, 0);
-  std::vector<double> cent(3 * (size_t)N);
-  for (long long i = 0; i < N; ++i) {
-    const double* p0 = &s.vertex_pos[3 * (size_t)s.vertex_idx[3 * i]];
-    const double* p1 = &s.vertex_pos[3 * (size_t)s.vertex_idx[3 * i + 1]];
-    const double* p2 = &s.vertex_pos[3 * (size_t)s.vertex_idx[3 * i + 2]];
-    for (int k = 0; k < 3; ++k) cent[3 * i + k] = (p0[k] + p1[k] + p2[k]) / 3.0;
-  }
-  auto update_bounds = [&](int node) {   // updateNodeBoundsSoA, mybvh.cpp:412-431
-    double mn[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, mx[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
-    const int f = b.first_tri[node], n = b.tri_count[node];
-    for (int i = f; i < f + n; ++i) {
-      for (int c = 0; c < 3; ++c) {
-        const double* p = &s.vertex_pos[3 * (size_t)s.vertex_idx[3 * (size_t)i + c]];
-        for (int k = 0; k < 3; ++k) { mn[k] = std::fmin(mn[k], p[k]); mx[k] = std::fmax(mx[k], p[k]); }
-      }
+// ---------------------------------------------------------------------------
+// BVH::initSoA's median-split builder (mybvh.cpp:375-539), parallel.
+// Subtrees own disjoint slot ranges, so they are built concurrently (one
+// thread per subtree down to a fixed depth), each into its own node arena with
+// local ids.  A final pass replays the reference's id allocation -- a node
+// allocates ids for its two children when it splits, children are processed
+// left first (LIFO, :456-468) -- so ids, bounds and the slot permutation are
+// bit-identical to the sequential build (tests/test_host_parity.py).
+namespace {
+
+struct FragNode {
+  double mn[3], mx[3];
+  int first = 0, count = 0;   // count > 0: leaf
+  int left = -1, right = -1;  // arena ids (internal)
+  int depth = 0;              // reference depth (root = 1), for the axis and the max-depth stat
+};
+
+struct BuildCtx {
+  SoA& s;
+  std::vector<double>& cent;
+  int par_levels;   // spawn a thread for the left subtree above this depth
+};
+
+void node_bounds(const SoA& s, FragNode& nd) {   // updateNodeBoundsSoA, mybvh.cpp:412-431
+  double mn[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, mx[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
+  for (int i = nd.first; i < nd.first + nd.count; ++i)
+    for (int c = 0; c < 3; ++c) {
+      const double* p = &s.vertex_pos[3 * (size_t)s.vertex_idx[3 * (size_t)i + c]];
+      for (int k = 0; k < 3; ++k) { mn[k] = std::fmin(mn[k], p[k]); mx[k] = std::fmax(mx[k], p[k]); }
     }
-    for (int k = 0; k < 3; ++k) { b.bb_min[3 * (size_t)node + k] = mn[k]; b.bb_max[3 * (size_t)node + k] = mx[k]; }
-  };
-  auto swap_slots = [&](size_t i, size_t j) {   // :497-503 (+ cached centroid)
-    for (int k = 0; k < 3; ++k) {
-      std::swap(s.face_normals[3 * i + k], s.face_normals[3 * j + k]);
-      std::swap(s.vertex_idx[3 * i + k], s.vertex_idx[3 * j + k]);
-      std::swap(s.texture_idx[3 * i + k], s.texture_idx[3 * j + k]);
-      std::swap(cent[3 * i + k], cent[3 * j + k]);
-    }
-  };
-  b.left_child[0] = 0; b.first_tri[0] = 0; b.tri_count[0] = (int)N;
-  int nodes_used = 1;
-  update_bounds(0);
+  for (int k = 0; k < 3; ++k) { nd.mn[k] = mn[k]; nd.mx[k] = mx[k]; }
+}
+
+// Splits arena[root] and its descendants (sequential within the subtree unless
+// depth < par_levels, where the left child's subtree goes to a new thread).
+void build_subtree(BuildCtx& cx, std::vector<FragNode>& arena, int root) {
   std::vector<double> axis_pts;
-  std::vector<std::pair<int, int>> stack;   // (node, depth)
-  stack.emplace_back(0, 1);
-  int maxd = 0;
+  std::vector<int> stack = {root};
   while (!stack.empty()) {
-    const auto [node, depth] = stack.back();
+    const int node = stack.back();
     stack.pop_back();
-    maxd = std::max(maxd, depth - 1);
-    const int n = b.tri_count[node];
+    const int n = arena[node].count, f = arena[node].first, depth = arena[node].depth;
     if (n <= 2) continue;                                    // :441
     const int axis = depth % 3;                              // :444
-    const int f = b.first_tri[node];
     axis_pts.resize(n);
-    for (int i = 0; i < n; ++i) axis_pts[i] = cent[3 * (size_t)(f + i) + axis];
-    // median_inplace, :346-362
-    const size_t mid = (size_t)n / 2;
+    for (int i = 0; i < n; ++i) axis_pts[i] = cx.cent[3 * (size_t)(f + i) + axis];
+    const size_t mid = (size_t)n / 2;                        // median_inplace, :346-362
     double split;
     std::nth_element(axis_pts.begin(), axis_pts.begin() + mid, axis_pts.end());
     if (n % 2 == 1) {
@@ -265,26 +259,125 @@ void build_bvh_soa(SoA& s, BvhSoA& b) {
     } else {
       const double hi = axis_pts[mid];
       std::nth_element(axis_pts.begin(), axis_pts.begin() + (mid - 1), axis_pts.begin() + mid);
-      const double lo = axis_pts[mid - 1];
-      split = 0.5 * (lo + hi);
+      split = 0.5 * (axis_pts[mid - 1] + hi);
     }
-    int i = f, j = f + n - 1;                                // :481-513
+    int i = f, j = f + n - 1;                                // :481-513 (+ cached centroids)
+    SoA& s = cx.s;
     while (i <= j) {
-      if (cent[3 * (size_t)i + axis] < split) { ++i; }
-      else { swap_slots((size_t)i, (size_t)j); --j; }
+      if (cx.cent[3 * (size_t)i + axis] < split) {
+        ++i;
+      } else {
+        for (int k = 0; k < 3; ++k) {
+          std::swap(s.face_normals[3 * (size_t)i + k], s.face_normals[3 * (size_t)j + k]);
+          std::swap(s.vertex_idx[3 * (size_t)i + k], s.vertex_idx[3 * (size_t)j + k]);
+          std::swap(s.texture_idx[3 * (size_t)i + k], s.texture_idx[3 * (size_t)j + k]);
+          std::swap(cx.cent[3 * (size_t)i + k], cx.cent[3 * (size_t)j + k]);
+        }
+        --j;
+      }
     }
     const int left_count = i - f;
     if (left_count == 0 || left_count == n) continue;        // :453
-    const int l = nodes_used, r = l + 1;                     // :456-464
+    FragNode l, r;
+    l.first = f; l.count = left_count; l.depth = depth + 1;
+    r.first = i; r.count = n - left_count; r.depth = depth + 1;
+    node_bounds(s, l);
+    node_bounds(s, r);
+    const int li = (int)arena.size();
+    arena.push_back(l);
+    arena.push_back(r);
+    arena[node].left = li;
+    arena[node].right = li + 1;
+    arena[node].count = 0;
+    if (depth < cx.par_levels) {   // left subtree on a new thread, right one here; then graft
+      std::vector<FragNode> sub = {arena[li]};
+      sub[0].left = sub[0].right = -1;
+      std::thread t([&cx, &sub]() { build_subtree(cx, sub, 0); });
+      build_subtree(cx, arena, li + 1);
+      t.join();
+      const int off = (int)arena.size() - 1;   // sub[k] (k >= 1) -> arena[off + k]; sub[0] -> arena[li]
+      auto remap = [&](int k) { return k <= 0 ? k : off + k; };
+      arena[li] = sub[0];
+      arena[li].left = remap(sub[0].left);
+      arena[li].right = remap(sub[0].right);
+      for (size_t k = 1; k < sub.size(); ++k) {
+        FragNode nd = sub[k];
+        nd.left = remap(nd.left);
+        nd.right = remap(nd.right);
+        arena.push_back(nd);
+      }
+      continue;
+    }
+    stack.push_back(li + 1);
+    stack.push_back(li);
+  }
+}
+
+int build_threads() {
+  const char* e = std::getenv("RT_BUILD_THREADS");
+  int t = e ? std::atoi(e) : 0;
+  if (t <= 0) {
+    const char* o = std::getenv("OMP_NUM_THREADS");
+    t = o ? std::atoi(o) : 0;
+  }
+  if (t <= 0) t = (int)std::thread::hardware_concurrency();
+  return std::max(1, std::min(t, 64));
+}
+
+}  // namespace
+
+void build_bvh_soa(SoA& s, BvhSoA& b) {
+  b = BvhSoA();
+  const long long N = s.n_vertex_idx / 3;
+  if (N <= 0) return;
+  std::vector<double> cent(3 * (size_t)N);
+  for (long long i = 0; i < N; ++i) {
+    const double* p0 = &s.vertex_pos[3 * (size_t)s.vertex_idx[3 * i]];
+    const double* p1 = &s.vertex_pos[3 * (size_t)s.vertex_idx[3 * i + 1]];
+    const double* p2 = &s.vertex_pos[3 * (size_t)s.vertex_idx[3 * i + 2]];
+    for (int k = 0; k < 3; ++k) cent[3 * i + k] = (p0[k] + p1[k] + p2[k]) / 3.0;
+  }
+  // threads = 2^par_levels; small builds stay sequential
+  int levels = 0;
+  const int threads = build_threads();
+  while ((1 << (levels + 1)) <= threads) ++levels;
+  if (N < 200000) levels = 0;
+  BuildCtx cx{s, cent, levels + 1};   // root depth is 1: split in parallel while depth <= levels
+  std::vector<FragNode> arena(1);
+  arena[0].first = 0;
+  arena[0].count = (int)N;
+  arena[0].depth = 1;
+  node_bounds(s, arena[0]);
+  build_subtree(cx, arena, 0);
+
+  // replay the reference's id allocation (children numbered at split time, left first)
+  const size_t cap = 2 * (size_t)N - 1;
+  b.bb_min.assign(3 * cap, 0.0);
+  b.bb_max.assign(3 * cap, 0.0);
+  b.left_child.assign(cap, 0);
+  b.first_tri.assign(cap, 0);
+  b.tri_count.assign(cap, 0);
+  int nodes_used = 1, maxd = 0;
+  std::vector<std::pair<int, int>> st = {{0, 0}};   // (arena id, reference id)
+  while (!st.empty()) {
+    const auto [a, id] = st.back();
+    st.pop_back();
+    const FragNode& nd = arena[a];
+    for (int k = 0; k < 3; ++k) { b.bb_min[3 * (size_t)id + k] = nd.mn[k]; b.bb_max[3 * (size_t)id + k] = nd.mx[k]; }
+    maxd = std::max(maxd, nd.depth - 1);
+    if (nd.left < 0) {
+      b.first_tri[id] = nd.first;
+      b.tri_count[id] = nd.count;
+      b.left_child[id] = 0;
+      continue;
+    }
+    const int l = nodes_used, r = l + 1;
     nodes_used += 2;
-    b.first_tri[l] = f; b.tri_count[l] = left_count;
-    b.first_tri[r] = i; b.tri_count[r] = n - left_count;
-    b.left_child[node] = l;
-    b.tri_count[node] = 0;
-    update_bounds(l);
-    update_bounds(r);
-    stack.emplace_back(r, depth + 1);
-    stack.emplace_back(l, depth + 1);
+    b.left_child[id] = l;
+    b.first_tri[id] = nd.first;   // the reference keeps firstTri of a split node (:457-464)
+    b.tri_count[id] = 0;
+    st.emplace_back(nd.right, r);
+    st.emplace_back(nd.left, l);
   }
   b.n_nodes = nodes_used;
   b.depth = maxd;

@@ -131,3 +131,20 @@ def test_bad_inputs_raise(tmp_path):
     bad.write_text("mesh x.obj WIREFRAME 0 0 0 0 0 0 0 0 0 1 0\n")
     with pytest.raises(rtamd.RtError):
         rtamd.HostScene.load(bad)
+
+
+def test_parallel_builder_is_bit_identical_to_sequential(monkeypatch):
+    # The median-split builder splits subtrees on threads and replays the reference's
+    # id allocation afterwards (host_scene.cpp build_bvh_soa): same tree, same permutation.
+    out = []
+    for threads in ("1", "8"):
+        monkeypatch.setenv("RT_BUILD_THREADS", threads)
+        hs = rtamd.HostScene.generate("random_tris", n_triangles=300_000, seed=7)
+        hs.prepare()
+        out.append((hs.bvh_arrays(), hs.soa_arrays(), hs.bvh_depth, hs))
+    (b1, s1, d1, _), (b8, s8, d8, _) = out
+    assert d1 == d8
+    for k in b1:
+        assert np.array_equal(b1[k], b8[k]), k
+    for k in ("vertex_idx", "face_normals", "texture_idx"):
+        assert np.array_equal(s1[k], s8[k]), k
