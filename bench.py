@@ -187,7 +187,8 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic: fixed-seed office_proxy stand-in (reference Office scene files are absent)",
+            "data": ("synthetic: fixed-seed office_proxy stand-in (reference Office scene files are absent)"
+                     if a.scene == "office" else f"synthetic: fixed-seed {a.scene} scene generator"),
             "config": {
                 "workload": f"{a.scene}_proxy {a.width}x{a.height} spp={a.spp * a.spp} depth={params.max_depth} "
                             f"lights={params.n_lights}",

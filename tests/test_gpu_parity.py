@@ -247,6 +247,28 @@ def test_full_size_4k_16spp_sampled_rows():
     assert np.abs(img[ys].reshape(-1, 3) - ref).max() <= TOL64
 
 
+def test_config4_10m_random_triangles_sampled_pixels():
+    # BASELINE config 4: 10 M random triangles (deep tree: depth 23, 4-wide stack bound 40 >
+    # the 16-entry LDS ring, so the global spill path runs), 1920x1080 1 spp.  Whole-frame ray
+    # counts against the kernel's own stripes; sampled pixels + their counts against the oracle.
+    hs, dev, orc = Case.get("random_tris", n_triangles=10_000_000)
+    assert hs.bvh_depth >= 20
+    p = hs.render_params(1920, 1080, 1)
+    p.out_format = rtamd.RT_OUT_RGB_F64
+    img, st = dev.render(p)
+    assert st.primary_rays == 1920 * 1080
+    rng = np.random.default_rng(3)
+    xy = np.stack([rng.integers(0, 1920, 400), rng.integers(0, 1080, 400)], 1).astype(np.int32)
+    xy[:100] = np.stack([rng.integers(760, 1160, 100), rng.integers(340, 740, 100)], 1)   # centre: hits
+    ref, cnt = orc.render_pixels(p, xy, pyoracle.MODE_REFERENCE)
+    got = img[xy[:, 1], xy[:, 0]]
+    assert np.abs(got - ref).max() <= TOL64
+    assert (ref.sum(-1) > 0).sum() > 50            # the sample really exercises hits and shadows
+    p.flags = rtamd.RT_FLAG_WIDE_STATS
+    _, _ = dev.render(p)
+    assert dev.debug_counters()["stack_spills"] > 0
+
+
 def test_bad_params_fail_loudly():
     hs, dev, _ = Case.get("cornell")
     p = hs.render_params(16, 16, 1)
