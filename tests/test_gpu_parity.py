@@ -269,6 +269,24 @@ def test_config4_10m_random_triangles_sampled_pixels():
     assert dev.debug_counters()["stack_spills"] > 0
 
 
+def test_config5_8k_64spp_one_of_8_shards_sampled_pixels():
+    # BASELINE config 5 (7680x4320, 8x8 stratified, rows sharded over 8 GPUs): the shard of
+    # rank 3 renders on this GPU; sampled pixels against the oracle at their global rows.
+    hs, dev, orc = Case.get("office")
+    p = hs.render_params(7680, 4320, 8)
+    p.stripe_height, p.stripe_count, p.stripe_index = 16, 8, 3
+    p.out_format = rtamd.RT_OUT_RGB_F64
+    img, st = dev.render(p)
+    rows = rtamd.shard_rows(4320, 16, 8, 3)
+    assert img.shape == (len(rows), 7680, 3) and st.primary_rays == len(rows) * 7680 * 64
+    rng = np.random.default_rng(11)
+    li = rng.integers(0, len(rows), 150)
+    xs = rng.integers(0, 7680, 150)
+    q = hs.render_params(7680, 4320, 8)
+    ref, _ = orc.render_pixels(q, np.stack([xs, rows[li]], 1).astype(np.int32), pyoracle.MODE_REFERENCE)
+    assert np.abs(img[li, xs] - ref).max() <= TOL64
+
+
 def test_bad_params_fail_loudly():
     hs, dev, _ = Case.get("cornell")
     p = hs.render_params(16, 16, 1)
