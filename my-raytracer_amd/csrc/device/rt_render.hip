@@ -275,6 +275,10 @@ __device__ __forceinline__ uint32_t u4c(const uint4& v, int c) {
   return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
 }
 
+#ifndef RT_SPECULATIVE
+#define RT_SPECULATIVE 1   // 4-wide: postponed leaves + speculative node traversal
+#endif
+
 #ifndef RT_WAVES_PER_EU
 #define RT_WAVES_PER_EU 4   // 4 waves/SIMD = 16 waves/CU (register budget 128 VGPRs)
 #endif
@@ -505,7 +509,72 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
       };
       const D3 c3 = d3(-rd.x, -rd.y, -rd.z);
 
-      while (__ballot(cur != kDone) != 0) {
+      // tests the triangles of leaf `lref` in record order; true = any-hit ray occluded
+      auto test_leaf = [&](uint32_t lref) -> bool {
+          // 2-wide: iterate reference slots in order (the oracle's order); 4-wide: device
+          // records of the (possibly refined) leaf.  Either way the hit kept is the
+          // smallest (t, slot), which does not depend on the order.
+          uint32_t i = lref & ~kLeaf;
+          const uint32_t leaf0 = i;
+          bool occluded = false;
+          for (;;) {
+            const uint32_t rec = (WIDTH == 2) ? P.slot2dev[i] : i;
+            if (STATS) {
+              c_tris++;
+              wave_tick(d_leaf_it, d_leaf_ln, lane);
+              wave_distinct((uint32_t)(((unsigned long long)i * sizeof(GTri)) >> 7), d_leaf_lines, lane);
+            }
+            const TriOps T = load_tri(P.tris, rec);
+            const int slot = (int)(T.meta & kSlotMask);
+            // Mesh::intersect_triangle (mymesh.cpp:190-215): the same fp64 S, Da, Db, Dt as
+            // the CPU (bit-identical operands and operation order).  Division-free early
+            // rejections first: they fire only where the CPU's rounded quotients certainly
+            // fail the same test (margins in DESIGN.md §4), so accept decisions are unchanged.
+            const D3 c4 = sub(ro, T.p2);
+            const double S = det3(T.e1, T.e2, c3);
+            if (fabs(S) >= 1e-10) {
+              const double Da = det3(c4, T.e2, c3);
+              const double Db = det3(T.e1, c4, c3);
+              const double sS = S > 0.0 ? 1.0 : -1.0;
+              const double aS = fabs(S);
+              const double ua = Da * sS, ub = Db * sS;                       // sign-normalised numerators
+              const double tiny = aS * 0x1p-1000, big = aS * (1.0 + 0x1p-48);
+              const bool out = (ua < 0.0 && -ua >= tiny) || (ub < 0.0 && -ub >= tiny) || ua > big || ub > big ||
+                               (Da + Db - S) * sS > 0x1p-40 * (fabs(Da) + fabs(Db) + aS);
+              if (!out) {
+                const double t = det3(T.e1, T.e2, c4) / S;
+                const bool cand = anyhit ? (t < tlim) : (t <= tlim);
+                if (t > 1e-5 && cand) {
+                  const double alpha = Da / S;
+                  const double beta = Db / S;
+                  const double gamma = (1.0 - alpha - beta);
+                  const bool inside = (0.0 <= alpha && alpha <= 1.0) && (0.0 <= beta && beta <= 1.0) &&
+                                      (0.0 <= gamma && gamma <= 1.0);
+                  if (inside) {
+                    if (anyhit) {
+                      shadow_hit = true;
+                      occluded = true;
+                      break;
+                    }
+                    if (t < tlim || slot < best_slot) {   // ties: smallest slot (mybvh.cpp:169 visit order)
+                      tlim = t;
+                      best = (int)rec;
+                      best_slot = slot;
+                      hi_c = round_up_f(tlim - t_off);
+                    }
+                  }
+                }
+              }
+            }
+            if (T.meta & (WIDTH == 2 ? kLastRef : kLastDev)) break;
+            ++i;
+          }
+          if (STATS && i - leaf0 + 1 > 4) d_big_leaf += i - leaf0 + 1;
+          return occluded;
+      };
+      uint32_t pleaf = kDone;   // 4-wide: postponed leaf
+
+      while (__ballot(cur != kDone || pleaf != kDone) != 0) {
         if (STATS) wave_tick(d_round_it, d_round_ln, lane);
         if constexpr (WIDTH == 2) {
         while (!(cur & kLeaf)) {   // internal node (kDone carries the leaf bit)
@@ -579,68 +648,40 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
             if (cnt > 1) push(v[1]);
             cur = v[0];
           }
-        }
-        }
-        if (cur != kDone) {   // leaf: test its triangles in slot order
-          // 2-wide: iterate reference slots in order (the oracle's order); 4-wide: device
-          // records of the (possibly refined) leaf.  Either way the hit kept is the
-          // smallest (t, slot), which does not depend on the order.
-          uint32_t i = cur & ~kLeaf;
-          const uint32_t leaf0 = i;
-          for (;;) {
-            const uint32_t rec = (WIDTH == 2) ? P.slot2dev[i] : i;
-            if (STATS) {
-              c_tris++;
-              wave_tick(d_leaf_it, d_leaf_ln, lane);
-              wave_distinct((uint32_t)(((unsigned long long)i * sizeof(GTri)) >> 7), d_leaf_lines, lane);
+          if (RT_SPECULATIVE) {
+            if ((cur & kLeaf) && cur != kDone && pleaf == kDone) {   // first leaf: postpone, keep going
+              pleaf = cur;
+              cur = pop();
             }
-            const TriOps T = load_tri(P.tris, rec);
-            const int slot = (int)(T.meta & kSlotMask);
-            // Mesh::intersect_triangle (mymesh.cpp:190-215): the same fp64 S, Da, Db, Dt as
-            // the CPU (bit-identical operands and operation order).  Division-free early
-            // rejections first: they fire only where the CPU's rounded quotients certainly
-            // fail the same test (margins in DESIGN.md §4), so accept decisions are unchanged.
-            const D3 c4 = sub(ro, T.p2);
-            const double S = det3(T.e1, T.e2, c3);
-            if (fabs(S) >= 1e-10) {
-              const double Da = det3(c4, T.e2, c3);
-              const double Db = det3(T.e1, c4, c3);
-              const double sS = S > 0.0 ? 1.0 : -1.0;
-              const double aS = fabs(S);
-              const double ua = Da * sS, ub = Db * sS;                       // sign-normalised numerators
-              const double tiny = aS * 0x1p-1000, big = aS * (1.0 + 0x1p-48);
-              const bool out = (ua < 0.0 && -ua >= tiny) || (ub < 0.0 && -ub >= tiny) || ua > big || ub > big ||
-                               (Da + Db - S) * sS > 0x1p-40 * (fabs(Da) + fabs(Db) + aS);
-              if (!out) {
-                const double t = det3(T.e1, T.e2, c4) / S;
-                const bool cand = anyhit ? (t < tlim) : (t <= tlim);
-                if (t > 1e-5 && cand) {
-                  const double alpha = Da / S;
-                  const double beta = Db / S;
-                  const double gamma = (1.0 - alpha - beta);
-                  const bool inside = (0.0 <= alpha && alpha <= 1.0) && (0.0 <= beta && beta <= 1.0) &&
-                                      (0.0 <= gamma && gamma <= 1.0);
-                  if (inside) {
-                    if (anyhit) {
-                      shadow_hit = true;
-                      cur = kDone;
-                      break;
-                    }
-                    if (t < tlim || slot < best_slot) {   // ties: smallest slot (mybvh.cpp:169 visit order)
-                      tlim = t;
-                      best = (int)rec;
-                      best_slot = slot;
-                      hi_c = round_up_f(tlim - t_off);
-                    }
-                  }
-                }
-              }
-            }
-            if (T.meta & (WIDTH == 2 ? kLastRef : kLastDev)) break;
-            ++i;
+            if (__ballot(pleaf == kDone && cur != kDone) == 0) break;   // every lane holds a leaf
           }
-          if (STATS && i - leaf0 + 1 > 4) d_big_leaf += i - leaf0 + 1;
-          if (cur != kDone) cur = pop();
+        }
+        }
+        // leaves: 2-wide -- the leaf the lane stopped at; 4-wide -- the postponed leaf, then
+        // any leaf the lane stopped at after it (chained), so lanes that found leaves early
+        // kept traversing instead of idling (speculative while-while, Aila & Laine 2009)
+        if constexpr (WIDTH == 2 || !RT_SPECULATIVE) {
+          if (cur != kDone) {
+            if (test_leaf(cur)) cur = kDone;
+            else cur = pop();
+          }
+        } else {
+          if (pleaf == kDone && cur != kDone) {   // stopped at a leaf without postponing one
+            pleaf = cur;
+            cur = pop();
+          }
+          while (pleaf != kDone) {
+            if (test_leaf(pleaf)) {   // any-hit: occluded, the ray is finished
+              cur = kDone;
+              pleaf = kDone;
+              break;
+            }
+            pleaf = kDone;
+            if ((cur & kLeaf) && cur != kDone) {
+              pleaf = cur;
+              cur = pop();
+            }
+          }
         }
       }
       thit = tlim;
