@@ -93,7 +93,7 @@ def main():
     params.stripe_count = n
     params.stripe_index = rank
     W = a.width
-    S = max(1, min(a.streams, 4))   # librt_hip keeps 4 launch contexts per scene
+    S = max(1, min(a.streams, 8))   # librt_hip keeps 8 launch contexts per scene
     bufs = [torch.zeros((shard_max_rows(a.height, STRIPE_H, n), W, 3), dtype=torch.float32, device="cuda")
             for _ in range(S)]
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(S - 1)]

@@ -152,7 +152,7 @@ int rt_rows_in_shard(const rt_render_params* p);
  * chosen format) on `stream` (hipStream_t, NULL = the null stream).
  * Asynchronous unless stats != NULL, in which case it synchronises the stream
  * and fills *stats.  Launches on different streams may run concurrently: the
- * scene keeps a ring of 4 launch contexts (path state, work heads, counters)
+ * scene keeps a ring of 8 launch contexts (path state, work heads, counters)
  * and a context is reused only after its previous launch completed.  Calls on
  * one scene must come from one host thread at a time.  Replaces launch_compute_image_device's primary pass
  * (mytracer_gpu.cu:66-81); the adaptive pass (:83-109) is SURVEY §8f "next". */

@@ -1132,7 +1132,7 @@ size_t lds_bytes(int stack_words) {
 // different streams can run concurrently: the drain of one frame (waves finishing
 // their last pixels) overlaps the next frame's work.  A context is
 // reused only after its previous launch completed (stream wait on `done`).
-constexpr int kContexts = 4;
+constexpr int kContexts = 8;
 struct LaunchCtx {
   unsigned long long* d_ctr = nullptr;       // [kCtrWords] work heads, stats, diagnostics
   double* d_pstate = nullptr;                // [nslots][kFields] path state
