@@ -1187,7 +1187,7 @@ int upload(T** dst, const std::vector<T>& src, long long& bytes) {
 }
 
 #ifndef RT_LEAF_MAX
-#define RT_LEAF_MAX 2
+#define RT_LEAF_MAX 1
 #endif
 constexpr int kLeafMax = RT_LEAF_MAX;   // device leaves hold at most this many triangles
 
