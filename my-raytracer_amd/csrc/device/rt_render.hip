@@ -91,6 +91,15 @@ __device__ __forceinline__ double buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t voff
 __device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, double x) {
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, x), r, voff, soff, 0);
 }
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 buf_ld4f(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
+  const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0u, 0);
+  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+__device__ __forceinline__ uint4 buf_ld4u(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
+  const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0u, 0);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
 
 // Lane of the k-th (0-based) set bit of m (k < popcount(m)).
 __device__ __forceinline__ int kth_set_bit(unsigned long long m, int k) {
@@ -134,7 +143,8 @@ struct KParams {
   size_t nslots;
   int n_gnodes;
   int out_fmt;
-  int pad0[2];
+  int n_gnodes4;
+  int pad0;
   double root_lo[3], root_hi[3];
   double eye[3], ll[3], xd[3], yd[3];
   int W, H;
@@ -269,6 +279,7 @@ struct RaySlots {
 //             global path state and write their next ray (if any) to LDS.
 // Nothing but a few ids is live across the phase boundary, which keeps the
 // kernel at 4 waves/SIMD despite fp64 shading.
+typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float f4c(const float4& v, int c) {
   return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
 }
@@ -278,6 +289,10 @@ __device__ __forceinline__ uint32_t u4c(const uint4& v, int c) {
 
 #ifndef RT_QNODE
 #define RT_QNODE 0   // 1: production traversal on quantised 64-B nodes (0: fp32 128-B nodes)
+#endif
+
+#ifndef RT_NODEOPT
+#define RT_NODEOPT 1   // 4-wide node visit: buffer loads, packed FMAs, branch-free pushes
 #endif
 
 #ifndef RT_SPECULATIVE
@@ -513,6 +528,8 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
         return spill[(size_t)sp * P.nslots];
       };
       const D3 c3 = d3(-rd.x, -rd.y, -rd.z);
+      const __amdgpu_buffer_rsrc_t nrs = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<GNode4*>(P.nodes4), 0, (int)((unsigned)P.n_gnodes4 * (unsigned)sizeof(GNode4)), kBufWord3);
 
       // tests the triangles of leaf `lref` in record order; true = any-hit ray occluded
       auto test_leaf = [&](uint32_t lref) -> bool {
@@ -640,6 +657,34 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
             const float tz0 = __builtin_fmaf((float)((nqz >> (8 * c)) & 255u), Az, Bz);
             const float tz1 = __builtin_fmaf((float)((fqz >> (8 * c)) & 255u), Az, Bz);
 #else
+#if RT_NODEOPT
+          // buffer loads: one 32-bit node offset, per-ray plane offsets added in 32 bits
+          const uint32_t nbo = cur * (uint32_t)sizeof(GNode4);
+          const float4 nx = buf_ld4f(nrs, nbo + nxo), fx = buf_ld4f(nrs, nbo + (nxo ^ 16u));
+          const float4 ny = buf_ld4f(nrs, nbo + nyo), fy = buf_ld4f(nrs, nbo + (nyo ^ 16u));
+          const float4 nz = buf_ld4f(nrs, nbo + nzo), fz = buf_ld4f(nrs, nbo + (nzo ^ 16u));
+          const uint4 rf = buf_ld4u(nrs, nbo + 96u);
+          // slabs two children at a time (v_pk_fma_f32, the scalar FMA's rounding)
+          const f2 ivx2 = {ivx, ivx}, ivy2 = {ivy, ivy}, ivz2 = {ivz, ivz};
+          const f2 mox2 = {-oix, -oix}, moy2 = {-oiy, -oiy}, moz2 = {-oiz, -oiz};
+          const f2 Tx0[2] = {__builtin_elementwise_fma(f2{nx.x, nx.y}, ivx2, mox2),
+                             __builtin_elementwise_fma(f2{nx.z, nx.w}, ivx2, mox2)};
+          const f2 Tx1[2] = {__builtin_elementwise_fma(f2{fx.x, fx.y}, ivx2, mox2),
+                             __builtin_elementwise_fma(f2{fx.z, fx.w}, ivx2, mox2)};
+          const f2 Ty0[2] = {__builtin_elementwise_fma(f2{ny.x, ny.y}, ivy2, moy2),
+                             __builtin_elementwise_fma(f2{ny.z, ny.w}, ivy2, moy2)};
+          const f2 Ty1[2] = {__builtin_elementwise_fma(f2{fy.x, fy.y}, ivy2, moy2),
+                             __builtin_elementwise_fma(f2{fy.z, fy.w}, ivy2, moy2)};
+          const f2 Tz0[2] = {__builtin_elementwise_fma(f2{nz.x, nz.y}, ivz2, moz2),
+                             __builtin_elementwise_fma(f2{nz.z, nz.w}, ivz2, moz2)};
+          const f2 Tz1[2] = {__builtin_elementwise_fma(f2{fz.x, fz.y}, ivz2, moz2),
+                             __builtin_elementwise_fma(f2{fz.z, fz.w}, ivz2, moz2)};
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const float tx0 = Tx0[c >> 1][c & 1], tx1 = Tx1[c >> 1][c & 1];
+            const float ty0 = Ty0[c >> 1][c & 1], ty1 = Ty1[c >> 1][c & 1];
+            const float tz0 = Tz0[c >> 1][c & 1], tz1 = Tz1[c >> 1][c & 1];
+#else
           const char* nb = reinterpret_cast<const char*>(P.nodes4) + (size_t)cur * sizeof(GNode4);
           const float4 nx = *reinterpret_cast<const float4*>(nb + nxo);
           const float4 fx = *reinterpret_cast<const float4*>(nb + (nxo ^ 16u));
@@ -653,6 +698,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
             const float tx0 = __builtin_fmaf(f4c(nx, c), ivx, -oix), tx1 = __builtin_fmaf(f4c(fx, c), ivx, -oix);
             const float ty0 = __builtin_fmaf(f4c(ny, c), ivy, -oiy), ty1 = __builtin_fmaf(f4c(fy, c), ivy, -oiy);
             const float tz0 = __builtin_fmaf(f4c(nz, c), ivz, -oiz), tz1 = __builtin_fmaf(f4c(fz, c), ivz, -oiz);
+#endif
 #endif
             const float tn = fmaxf(fmaxf(tx0, ty0), fmaxf(tz0, lo_c));
             const float tf = fminf(fminf(tx1, ty1), fminf(tz1, hi_c));
@@ -671,6 +717,13 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
 #undef RT_CSWAP
           if (cnt == 0) {
             cur = pop();
+          } else if (RT_NODEOPT && sp - slo + 3 <= kShortStack) {   // room for 3: branch-free pushes
+            const int np = cnt - 1;                                  // far-first: v[np] .. v[1]
+            stk[(sp & kStackMask) * kBlock] = np == 3 ? v[3] : (np == 2 ? v[2] : v[1]);
+            stk[((sp + 1) & kStackMask) * kBlock] = np == 3 ? v[2] : v[1];
+            stk[((sp + 2) & kStackMask) * kBlock] = v[1];
+            sp += np;
+            cur = v[0];
           } else {
             if (cnt > 3) push(v[3]);
             if (cnt > 2) push(v[2]);
@@ -1725,6 +1778,7 @@ int launch_render(rt_scene* sc, const rt_render_params* p, void* d_out, rt_stats
   P.ctr = C.d_ctr;
   P.out = d_out;
   P.n_gnodes = sc->n_gnodes;
+  P.n_gnodes4 = sc->n_gnodes4;
   P.out_fmt = p->out_format;
   for (int k = 0; k < 3; ++k) {
     P.root_lo[k] = sc->root_lo[k]; P.root_hi[k] = sc->root_hi[k];
