@@ -59,20 +59,6 @@ constexpr uint32_t kSlotMask = 0x3fffffffu;
 constexpr uint32_t kLastRef = 0x40000000u;   // slot is the last of its reference leaf
 constexpr uint32_t kLastDev = 0x80000000u;   // record is the last of its device leaf
 
-// Quantised 4-wide node (64 B = 4 x dwordx4): the same children as GNode4 with
-// their fp32 boxes re-expressed on an 8-bit grid anchored at the union box's low
-// corner: plane = origin + q * scale (scale a power of two), q rounded outward
-// (lo down, hi up), so every decoded box contains the fp32 box.
-// Absent children: qlo = 255, qhi = 0 (empty interval) and ref = kEmpty.
-struct alignas(64) GNode4Q {
-  float ox, oy, oz, sx;            // origin, scale x
-  float sy, sz;                    // scale y, z
-  uint32_t qlo_x, qhi_x;           // byte c = child c
-  uint32_t qlo_y, qhi_y, qlo_z, qhi_z;
-  uint32_t ref[4];
-};
-static_assert(sizeof(GNode4Q) == 64, "GNode4Q must be 64 bytes");
-
 struct alignas(16) GTri {
   double e1[3];
   double e2[3];

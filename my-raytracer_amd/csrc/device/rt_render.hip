@@ -85,21 +85,16 @@ __device__ __forceinline__ void wave_lds_sync() {
 // Raw buffer access (gfx9 resource word 3; no format conversion).
 constexpr int kBufWord3 = 0x00020000;
 typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+#ifndef RT_PS_AUX
+#define RT_PS_AUX 0   // cache policy bits of path-state accesses (experiment: 2 = nt)
+#endif
 __device__ __forceinline__ double buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, RT_PS_AUX));
 }
 __device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, double x) {
-  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, x), r, voff, soff, 0);
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, x), r, voff, soff, RT_PS_AUX);
 }
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ float4 buf_ld4f(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
-  const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0u, 0);
-  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
-}
-__device__ __forceinline__ uint4 buf_ld4u(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
-  const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0u, 0);
-  return make_uint4(v.x, v.y, v.z, v.w);
-}
+
 
 // Lane of the k-th (0-based) set bit of m (k < popcount(m)).
 __device__ __forceinline__ int kth_set_bit(unsigned long long m, int k) {
@@ -124,7 +119,6 @@ constexpr unsigned kGuardIters = 1u << 24;   // persistent-loop watchdog (never 
 struct KParams {
   const GNode* nodes;
   const GNode4* nodes4;
-  const GNode4Q* nodes4q;
   const GTri* tris;
   const uint32_t* slot2dev; // reference slot -> device record (2-wide canonical kernel)
   const TriShade* shade;
@@ -143,8 +137,7 @@ struct KParams {
   size_t nslots;
   int n_gnodes;
   int out_fmt;
-  int n_gnodes4;
-  int pad0;
+  int pad0[2];
   double root_lo[3], root_hi[3];
   double eye[3], ll[3], xd[3], yd[3];
   int W, H;
@@ -279,21 +272,12 @@ struct RaySlots {
 //             global path state and write their next ray (if any) to LDS.
 // Nothing but a few ids is live across the phase boundary, which keeps the
 // kernel at 4 waves/SIMD despite fp64 shading.
-typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float f4c(const float4& v, int c) {
   return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
 }
 __device__ __forceinline__ uint32_t u4c(const uint4& v, int c) {
   return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
 }
-
-#ifndef RT_QNODE
-#define RT_QNODE 0   // 1: production traversal on quantised 64-B nodes (0: fp32 128-B nodes)
-#endif
-
-#ifndef RT_NODEOPT
-#define RT_NODEOPT 1   // 4-wide node visit: buffer loads, packed FMAs, branch-free pushes
-#endif
 
 #ifndef RT_SPECULATIVE
 #define RT_SPECULATIVE 1   // 4-wide: postponed leaves + speculative node traversal
@@ -528,8 +512,6 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
         return spill[(size_t)sp * P.nslots];
       };
       const D3 c3 = d3(-rd.x, -rd.y, -rd.z);
-      const __amdgpu_buffer_rsrc_t nrs = __builtin_amdgcn_make_buffer_rsrc(
-          const_cast<GNode4*>(P.nodes4), 0, (int)((unsigned)P.n_gnodes4 * (unsigned)sizeof(GNode4)), kBufWord3);
 
       // tests the triangles of leaf `lref` in record order; true = any-hit ray occluded
       auto test_leaf = [&](uint32_t lref) -> bool {
@@ -634,57 +616,6 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
           float k[4];
           uint32_t v[4];
           int cnt = 0;
-#if RT_QNODE
-          // quantised node: t = q * (scale * inv) + (origin * inv - o * inv); the scale is a
-          // power of two, so scale*inv is exact and the error is that of the fp32 FMA form
-          const float4* nq = reinterpret_cast<const float4*>(P.nodes4q + cur);
-          const float4 a0 = nq[0], a1 = nq[1];
-          const uint4 qy = *reinterpret_cast<const uint4*>(nq + 2);
-          const uint4 rf = *reinterpret_cast<const uint4*>(nq + 3);
-          const float Ax = ivx * a0.w, Ay = ivy * a1.x, Az = ivz * a1.y;
-          const float Bx = __builtin_fmaf(a0.x, ivx, -oix), By = __builtin_fmaf(a0.y, ivy, -oiy),
-                      Bz = __builtin_fmaf(a0.z, ivz, -oiz);
-          const uint32_t qlx = __float_as_uint(a1.z), qhx = __float_as_uint(a1.w);
-          const uint32_t nqx = nxo ? qhx : qlx, fqx = nxo ? qlx : qhx;
-          const uint32_t nqy = nyo != 32u ? qy.y : qy.x, fqy = nyo != 32u ? qy.x : qy.y;
-          const uint32_t nqz = nzo != 64u ? qy.w : qy.z, fqz = nzo != 64u ? qy.z : qy.w;
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const float tx0 = __builtin_fmaf((float)((nqx >> (8 * c)) & 255u), Ax, Bx);
-            const float tx1 = __builtin_fmaf((float)((fqx >> (8 * c)) & 255u), Ax, Bx);
-            const float ty0 = __builtin_fmaf((float)((nqy >> (8 * c)) & 255u), Ay, By);
-            const float ty1 = __builtin_fmaf((float)((fqy >> (8 * c)) & 255u), Ay, By);
-            const float tz0 = __builtin_fmaf((float)((nqz >> (8 * c)) & 255u), Az, Bz);
-            const float tz1 = __builtin_fmaf((float)((fqz >> (8 * c)) & 255u), Az, Bz);
-#else
-#if RT_NODEOPT
-          // buffer loads: one 32-bit node offset, per-ray plane offsets added in 32 bits
-          const uint32_t nbo = cur * (uint32_t)sizeof(GNode4);
-          const float4 nx = buf_ld4f(nrs, nbo + nxo), fx = buf_ld4f(nrs, nbo + (nxo ^ 16u));
-          const float4 ny = buf_ld4f(nrs, nbo + nyo), fy = buf_ld4f(nrs, nbo + (nyo ^ 16u));
-          const float4 nz = buf_ld4f(nrs, nbo + nzo), fz = buf_ld4f(nrs, nbo + (nzo ^ 16u));
-          const uint4 rf = buf_ld4u(nrs, nbo + 96u);
-          // slabs two children at a time (v_pk_fma_f32, the scalar FMA's rounding)
-          const f2 ivx2 = {ivx, ivx}, ivy2 = {ivy, ivy}, ivz2 = {ivz, ivz};
-          const f2 mox2 = {-oix, -oix}, moy2 = {-oiy, -oiy}, moz2 = {-oiz, -oiz};
-          const f2 Tx0[2] = {__builtin_elementwise_fma(f2{nx.x, nx.y}, ivx2, mox2),
-                             __builtin_elementwise_fma(f2{nx.z, nx.w}, ivx2, mox2)};
-          const f2 Tx1[2] = {__builtin_elementwise_fma(f2{fx.x, fx.y}, ivx2, mox2),
-                             __builtin_elementwise_fma(f2{fx.z, fx.w}, ivx2, mox2)};
-          const f2 Ty0[2] = {__builtin_elementwise_fma(f2{ny.x, ny.y}, ivy2, moy2),
-                             __builtin_elementwise_fma(f2{ny.z, ny.w}, ivy2, moy2)};
-          const f2 Ty1[2] = {__builtin_elementwise_fma(f2{fy.x, fy.y}, ivy2, moy2),
-                             __builtin_elementwise_fma(f2{fy.z, fy.w}, ivy2, moy2)};
-          const f2 Tz0[2] = {__builtin_elementwise_fma(f2{nz.x, nz.y}, ivz2, moz2),
-                             __builtin_elementwise_fma(f2{nz.z, nz.w}, ivz2, moz2)};
-          const f2 Tz1[2] = {__builtin_elementwise_fma(f2{fz.x, fz.y}, ivz2, moz2),
-                             __builtin_elementwise_fma(f2{fz.z, fz.w}, ivz2, moz2)};
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const float tx0 = Tx0[c >> 1][c & 1], tx1 = Tx1[c >> 1][c & 1];
-            const float ty0 = Ty0[c >> 1][c & 1], ty1 = Ty1[c >> 1][c & 1];
-            const float tz0 = Tz0[c >> 1][c & 1], tz1 = Tz1[c >> 1][c & 1];
-#else
           const char* nb = reinterpret_cast<const char*>(P.nodes4) + (size_t)cur * sizeof(GNode4);
           const float4 nx = *reinterpret_cast<const float4*>(nb + nxo);
           const float4 fx = *reinterpret_cast<const float4*>(nb + (nxo ^ 16u));
@@ -698,8 +629,6 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
             const float tx0 = __builtin_fmaf(f4c(nx, c), ivx, -oix), tx1 = __builtin_fmaf(f4c(fx, c), ivx, -oix);
             const float ty0 = __builtin_fmaf(f4c(ny, c), ivy, -oiy), ty1 = __builtin_fmaf(f4c(fy, c), ivy, -oiy);
             const float tz0 = __builtin_fmaf(f4c(nz, c), ivz, -oiz), tz1 = __builtin_fmaf(f4c(fz, c), ivz, -oiz);
-#endif
-#endif
             const float tn = fmaxf(fmaxf(tx0, ty0), fmaxf(tz0, lo_c));
             const float tf = fminf(fminf(tx1, ty1), fminf(tz1, hi_c));
             const uint32_t r = u4c(rf, c);
@@ -717,13 +646,6 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
 #undef RT_CSWAP
           if (cnt == 0) {
             cur = pop();
-          } else if (RT_NODEOPT && sp - slo + 3 <= kShortStack) {   // room for 3: branch-free pushes
-            const int np = cnt - 1;                                  // far-first: v[np] .. v[1]
-            stk[(sp & kStackMask) * kBlock] = np == 3 ? v[3] : (np == 2 ? v[2] : v[1]);
-            stk[((sp + 1) & kStackMask) * kBlock] = np == 3 ? v[2] : v[1];
-            stk[((sp + 2) & kStackMask) * kBlock] = v[1];
-            sp += np;
-            cur = v[0];
           } else {
             if (cnt > 3) push(v[3]);
             if (cnt > 2) push(v[2]);
@@ -1254,7 +1176,6 @@ struct rt_scene {
   int n_cu = 0;
   int blocks_per_cu[kNumVariants] = {0, 0, 0};
   GNode4* d_nodes4 = nullptr;
-  GNode4Q* d_nodes4q = nullptr;
   int n_gnodes4 = 0;
 };
 
@@ -1359,49 +1280,6 @@ void build_device_tree(const rt_scene_soa* s, const rt_bvh_soa* b, DevTree& E, s
       refine(id, b->first_tri[n], b->tri_count[n]);
     }
   }
-}
-
-// GNode4 -> GNode4Q: per axis, origin = union low corner (fp32), scale = the
-// smallest power of two with 255 * scale >= extent; child planes rounded outward
-// onto the grid (exact in double), so the decoded box contains the fp32 box.
-GNode4Q quantise_node(const GNode4& g) {
-  GNode4Q q;
-  std::memset(&q, 0, sizeof q);
-  const float* lo[3] = {g.lox, g.loy, g.loz};
-  const float* hi[3] = {g.hix, g.hiy, g.hiz};
-  float org[3], scl[3];
-  uint32_t qlo[3] = {0, 0, 0}, qhi[3] = {0, 0, 0};
-  for (int k = 0; k < 3; ++k) {
-    float plo = INFINITY, phi = -INFINITY;
-    for (int c = 0; c < 4; ++c)
-      if (g.ref[c] != kEmpty) { plo = std::min(plo, lo[k][c]); phi = std::max(phi, hi[k][c]); }
-    if (!(plo <= phi)) { plo = 0.f; phi = 0.f; }
-    const double ext = (double)phi - (double)plo;
-    double s = 1.0;
-    if (ext > 0.0) {
-      int e = 0;
-      std::frexp(ext / 255.0, &e);   // ext/255 <= 2^e
-      s = std::ldexp(1.0, e);
-    }
-    org[k] = plo;
-    scl[k] = (float)s;
-    for (int c = 0; c < 4; ++c) {
-      uint32_t a = 255u, b = 0u;   // empty interval
-      if (g.ref[c] != kEmpty) {
-        const double fl = std::floor(((double)lo[k][c] - (double)plo) / s);
-        const double ce = std::ceil(((double)hi[k][c] - (double)plo) / s);
-        a = (uint32_t)std::min(255.0, std::max(0.0, fl));
-        b = (uint32_t)std::min(255.0, std::max(0.0, ce));
-      }
-      qlo[k] |= a << (8 * c);
-      qhi[k] |= b << (8 * c);
-    }
-  }
-  q.ox = org[0]; q.oy = org[1]; q.oz = org[2];
-  q.sx = scl[0]; q.sy = scl[1]; q.sz = scl[2];
-  q.qlo_x = qlo[0]; q.qhi_x = qhi[0]; q.qlo_y = qlo[1]; q.qhi_y = qhi[1]; q.qlo_z = qlo[2]; q.qhi_z = qhi[2];
-  for (int c = 0; c < 4; ++c) q.ref[c] = g.ref[c];
-  return q;
 }
 
 int validate(const rt_scene_soa* s, const rt_bvh_soa* b) {
@@ -1598,10 +1476,6 @@ int rt_scene_upload(const rt_scene_soa* s, const rt_bvh_soa* b, int device, rt_s
     }
   }
 
-  // ---- quantised copy of the 4-wide nodes (RT_QNODE layout) ----
-  std::vector<GNode4Q> nodes4q(nodes4.size());
-  for (size_t gi = 0; gi < nodes4.size(); ++gi) nodes4q[gi] = quantise_node(nodes4[gi]);
-
   if (depth > kMaxDepth || stack4 > kMaxDepth)
     return fail(RT_ERR_UNSUPPORTED, "rt_scene_upload: BVH needs more than 4096 traversal-stack entries");
 
@@ -1664,7 +1538,6 @@ int rt_scene_upload(const rt_scene_soa* s, const rt_bvh_soa* b, int device, rt_s
   rc = RT_OK;
   if (rc == RT_OK) rc = upload(&sc->d_nodes, nodes, bytes);
   if (rc == RT_OK) rc = upload(&sc->d_nodes4, nodes4, bytes);
-  if (rc == RT_OK) rc = upload(&sc->d_nodes4q, nodes4q, bytes);
   if (rc == RT_OK) rc = upload(&sc->d_tris, tris, bytes);
   if (rc == RT_OK) rc = upload(&sc->d_slot2dev, slot2dev, bytes);
   if (rc == RT_OK) rc = upload(&sc->d_shade, shade, bytes);
@@ -1771,14 +1644,13 @@ int launch_render(rt_scene* sc, const rt_render_params* p, void* d_out, rt_stats
 
   KParams P;
   std::memset(&P, 0, sizeof P);
-  P.nodes = sc->d_nodes; P.nodes4 = sc->d_nodes4; P.nodes4q = sc->d_nodes4q; P.tris = sc->d_tris; P.slot2dev = sc->d_slot2dev; P.shade = sc->d_shade; P.fnorm = sc->d_fnorm;
+  P.nodes = sc->d_nodes; P.nodes4 = sc->d_nodes4; P.tris = sc->d_tris; P.slot2dev = sc->d_slot2dev; P.shade = sc->d_shade; P.fnorm = sc->d_fnorm;
   P.vnorm = sc->d_vnorm; P.tu = sc->d_tu; P.tv = sc->d_tv; P.texels = sc->d_texels; P.mats = sc->d_mats;
   LaunchCtx& C = sc->ctx[sc->next_ctx];
   const int ci = sc->next_ctx;
   P.ctr = C.d_ctr;
   P.out = d_out;
   P.n_gnodes = sc->n_gnodes;
-  P.n_gnodes4 = sc->n_gnodes4;
   P.out_fmt = p->out_format;
   for (int k = 0; k < 3; ++k) {
     P.root_lo[k] = sc->root_lo[k]; P.root_hi[k] = sc->root_hi[k];
@@ -1967,7 +1839,7 @@ void rt_scene_free(rt_scene* sc) {
   if (!sc) return;
   (void)hipSetDevice(sc->device);
   (void)hipDeviceSynchronize();   // launches may still be reading the scene
-  void* ptrs[] = {sc->d_nodes, sc->d_nodes4, sc->d_nodes4q, sc->d_tris, sc->d_shade, sc->d_fnorm, sc->d_vnorm, sc->d_tu,
+  void* ptrs[] = {sc->d_nodes, sc->d_nodes4, sc->d_tris, sc->d_shade, sc->d_fnorm, sc->d_vnorm, sc->d_tu,
                   sc->d_tv, sc->d_texels, sc->d_mats, sc->d_lights, sc->d_slot2dev};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
