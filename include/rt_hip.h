@@ -145,6 +145,17 @@ int rt_scene_upload(const rt_scene_soa* soa, const rt_bvh_soa* bvh, int device, 
 /* Device bytes held by the scene (nodes, triangles, shading data). */
 long long rt_scene_device_bytes(const rt_scene* scene);
 
+/* Opt-in analytic primitives: the spheres and planes of the
+ * raw scene (rt_raw_scene.spheres / .planes), tested in fp64 before the BVH in
+ * the CPU's order -- spheres, then planes, nearest strictly closer wins, then
+ * triangles only if strictly closer (oracle intersect_scene; Sphere/Plane
+ * intersect, myplane.cpp:22-49).  The reference GPU path traces meshes only
+ * (intersect_scene_device, mytracer_gpu.cu:314-328); a scene without this call
+ * matches it.  Replaces
+ * any previous set; n = 0 removes them.  Synchronises the device. */
+int rt_scene_set_analytic(rt_scene* scene, const rt_sphere* spheres, int n_spheres, const rt_plane* planes,
+                          int n_planes);
+
 /* Number of rows rt_launch_compute_image writes for these params. */
 int rt_rows_in_shard(const rt_render_params* p);
 

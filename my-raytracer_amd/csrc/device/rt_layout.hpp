@@ -28,6 +28,7 @@ constexpr uint32_t kLeaf = 0x80000000u;
 constexpr uint32_t kEmpty = 0x7fffffffu;
 constexpr uint32_t kDone = 0xffffffffu;
 constexpr int kNoHit = 0x7fffffff;
+constexpr int kPrimHit = 0x40000000;   // best = kPrimHit | k: analytic primitive k (never a triangle record)
 
 struct alignas(64) GNode {
   float x[4];   // lo0, hi0, lo1, hi1
@@ -89,5 +90,17 @@ struct alignas(16) GMat {
   int64_t pad;
 };
 static_assert(sizeof(GMat) == 128, "GMat must be 128 bytes");
+
+// Analytic primitive (opt-in, rt_scene_set_analytic): spheres first, then planes, each in
+// scene order -- the order intersect_scene tests them (oracle/rt_oracle.c intersect_scene).
+enum : int32_t { kPrimSphere = 0, kPrimPlane = 1 };
+struct alignas(16) GPrim {
+  double c[3];      // sphere centre / point on the plane
+  double r;         // sphere radius (unused for planes)
+  double n[3];      // plane unit normal (unused for spheres)
+  int32_t type;     // kPrimSphere / kPrimPlane
+  int32_t mat;      // index into the material table (after the meshes' materials)
+};
+static_assert(sizeof(GPrim) == 64, "GPrim must be 64 bytes");
 
 }  // namespace rtk

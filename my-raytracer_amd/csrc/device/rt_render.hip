@@ -155,7 +155,8 @@ struct KParams {
   const unsigned long long* list_count;
   double* sample_out;
   int nsamp;
-  int pad2;
+  int n_prims;              // analytic primitives (0 unless rt_scene_set_analytic)
+  const GPrim* prims;
 };
 
 // ---- fp64 vector ops (course vec4 semantics on xyz) ----
@@ -180,6 +181,31 @@ __device__ __forceinline__ double stdmin(double a, double b) { return (b < a) ? 
 __device__ __forceinline__ double det3(D3 v1, D3 v2, D3 v3) {
   return v1.x * (v2.y * v3.z - v3.y * v2.z) - v2.x * (v1.y * v3.z - v3.y * v1.z) +
          v3.x * (v1.y * v2.z - v2.y * v1.z);
+}
+
+// Analytic hits in fp64, the oracle's operation order (oracle/rt_oracle.c plane_hit /
+// sphere_hit, myplane.cpp:22-49); returns the hit distance or DBL_MAX.
+__device__ __forceinline__ double prim_hit(const GPrim& G, D3 o, D3 d) {
+  const D3 c = d3(G.c[0], G.c[1], G.c[2]);
+  if (G.type == kPrimPlane) {
+    const D3 n = d3(G.n[0], G.n[1], G.n[2]);
+    const double cos_theta = dot(n, d);
+    if (fabs(cos_theta) < 1e-9) return DBL_MAX;
+    const double t = (dot(n, c) - dot(n, o)) / cos_theta;
+    return t > 1e-5 ? t : DBL_MAX;
+  }
+  const D3 oc = sub(o, c);
+  const double a = dot(d, d);
+  const double b = 2.0 * dot(d, oc);
+  const double cc = dot(oc, oc) - G.r * G.r;
+  const double disc = b * b - 4.0 * a * cc;
+  if (disc < 0.0) return DBL_MAX;
+  const double sq = sqrt(disc);
+  const double t1 = (-b - sq) / (2.0 * a), t2 = (-b + sq) / (2.0 * a);
+  double t = DBL_MAX;
+  if (t1 > 1e-5 && t1 < t) t = t1;
+  if (t2 > 1e-5 && t2 < t) t = t2;
+  return t;
 }
 
 __device__ __forceinline__ float next_up(float f) {
@@ -444,7 +470,20 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
       shadow_hit = false;
       uint32_t cur = kDone;
       double t_off = 0.0;
-      if (busy && P.n_gnodes > 0) {   // conservative fp32 box ray (oracle/rt_oracle.c gray_setup)
+      // analytic primitives first, in scene order (oracle/rt_oracle.c intersect_scene /
+      // shadowed): a hit sets the running best with slot -1, so only a strictly closer
+      // triangle replaces it; a shadow ray they block skips the BVH.
+      for (int k = 0; k < P.n_prims; ++k) {
+        if (!busy) break;
+        const double t = prim_hit(P.prims[k], ro, rd);
+        if (t < tlim) {
+          if (anyhit) { shadow_hit = true; break; }
+          tlim = t;
+          best = kPrimHit | k;
+          best_slot = -1;
+        }
+      }
+      if (busy && P.n_gnodes > 0 && !shadow_hit) {   // conservative fp32 box ray (oracle/rt_oracle.c gray_setup)
         bool miss = false;
         const double o3[3] = {ro.x, ro.y, ro.z}, d3v[3] = {rd.x, rd.y, rd.z};
         bool inside = true;
@@ -796,44 +835,55 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
           // hit attributes: mymesh.cpp:217-235 (texture :70-95)
           const D3 ro = d3(*R.o[0], *R.o[1], *R.o[2]);
           const D3 rd = d3(*R.d[0], *R.d[1], *R.d[2]);
-          const TriOps T = load_tri(P.tris, (uint32_t)best);
           const D3 c3 = d3(-rd.x, -rd.y, -rd.z);
-          const D3 c4 = sub(ro, T.p2);
-          const double S = det3(T.e1, T.e2, c3);
-          const double alpha = det3(c4, T.e2, c3) / S;
-          const double beta = det3(T.e1, c4, c3) / S;
-          const double gamma = (1.0 - alpha - beta);
           hp = add(ro, scl(thit, rd));
           hview = c3;
-          mesh = T.mesh;
+          D3 hdiff;
+          if (best & kPrimHit) {   // analytic hit (oracle/rt_oracle.c intersect_scene): no texture
+            const GPrim& G = P.prims[best & (kPrimHit - 1)];
+            hn = G.type == kPrimPlane ? d3(G.n[0], G.n[1], G.n[2])
+                                      : d3((ro.x + thit * rd.x - G.c[0]) / G.r, (ro.y + thit * rd.y - G.c[1]) / G.r,
+                                           (ro.z + thit * rd.z - G.c[2]) / G.r);
+            mesh = G.mat;
+            const GMat& Mp = P.mats[mesh];
+            hdiff = d3(Mp.kd[0], Mp.kd[1], Mp.kd[2]);
+          } else {
+            const TriOps T = load_tri(P.tris, (uint32_t)best);
+            const D3 c4 = sub(ro, T.p2);
+            const double S = det3(T.e1, T.e2, c3);
+            const double alpha = det3(c4, T.e2, c3) / S;
+            const double beta = det3(T.e1, c4, c3) / S;
+            const double gamma = (1.0 - alpha - beta);
+            mesh = T.mesh;
+            const GMat& Mt = P.mats[mesh];
+            if (Mt.draw_mode == RT_DRAW_FLAT) {
+              const double* fnp = P.fnorm + 3 * (size_t)best;
+              hn = d3(fnp[0], fnp[1], fnp[2]);
+            } else {
+              const TriShade sh = P.shade[best];
+              const double* n0 = P.vnorm + 3 * (size_t)sh.v[0];
+              const double* n1 = P.vnorm + 3 * (size_t)sh.v[1];
+              const double* n2 = P.vnorm + 3 * (size_t)sh.v[2];
+              hn = d3(alpha * n0[0] + beta * n1[0] + gamma * n2[0], alpha * n0[1] + beta * n1[1] + gamma * n2[1],
+                      alpha * n0[2] + beta * n1[2] + gamma * n2[2]);
+            }
+            if (Mt.tex_w > 0) {
+              const TriShade sh = P.shade[best];
+              double u = alpha * P.tu[sh.t[0]] + beta * P.tu[sh.t[1]] + gamma * P.tu[sh.t[2]];
+              double v = alpha * P.tv[sh.t[0]] + beta * P.tv[sh.t[1]] + gamma * P.tv[sh.t[2]];
+              u = u < 0.0 ? 0.0 : (1.0 < u ? 1.0 : u);
+              v = v < 0.0 ? 0.0 : (1.0 < v ? 1.0 : v);
+              const unsigned TW = (unsigned)Mt.tex_w, TH = (unsigned)Mt.tex_h;
+              const int tx = (int)round(u * (TW - 1));
+              const int ty = (int)round((1.0 - v) * (TH - 1));
+              const unsigned char* t3 = P.texels + 3 * (Mt.tex_off + (long long)ty * TW + tx);
+              hdiff = d3((double)t3[0] / 255.0, (double)t3[1] / 255.0, (double)t3[2] / 255.0);
+            } else {
+              hdiff = d3(Mt.kd[0], Mt.kd[1], Mt.kd[2]);
+            }
+          }
           const GMat& M = P.mats[mesh];
           mirror = M.mirror;
-          if (M.draw_mode == RT_DRAW_FLAT) {
-            const double* fnp = P.fnorm + 3 * (size_t)best;
-            hn = d3(fnp[0], fnp[1], fnp[2]);
-          } else {
-            const TriShade sh = P.shade[best];
-            const double* n0 = P.vnorm + 3 * (size_t)sh.v[0];
-            const double* n1 = P.vnorm + 3 * (size_t)sh.v[1];
-            const double* n2 = P.vnorm + 3 * (size_t)sh.v[2];
-            hn = d3(alpha * n0[0] + beta * n1[0] + gamma * n2[0], alpha * n0[1] + beta * n1[1] + gamma * n2[1],
-                    alpha * n0[2] + beta * n1[2] + gamma * n2[2]);
-          }
-          D3 hdiff;
-          if (M.tex_w > 0) {
-            const TriShade sh = P.shade[best];
-            double u = alpha * P.tu[sh.t[0]] + beta * P.tu[sh.t[1]] + gamma * P.tu[sh.t[2]];
-            double v = alpha * P.tv[sh.t[0]] + beta * P.tv[sh.t[1]] + gamma * P.tv[sh.t[2]];
-            u = u < 0.0 ? 0.0 : (1.0 < u ? 1.0 : u);
-            v = v < 0.0 ? 0.0 : (1.0 < v ? 1.0 : v);
-            const unsigned TW = (unsigned)M.tex_w, TH = (unsigned)M.tex_h;
-            const int tx = (int)round(u * (TW - 1));
-            const int ty = (int)round((1.0 - v) * (TH - 1));
-            const unsigned char* t3 = P.texels + 3 * (M.tex_off + (long long)ty * TW + tx);
-            hdiff = d3((double)t3[0] / 255.0, (double)t3[1] / 255.0, (double)t3[2] / 255.0);
-          } else {
-            hdiff = d3(M.kd[0], M.kd[1], M.kd[2]);
-          }
           // ambient term (mytracer.cpp:574-576)
           D3 lacc = d3(0.0 + P.amb[0] * M.ka[0], 0.0 + P.amb[1] * M.ka[1], 0.0 + P.amb[2] * M.ka[2]);
           light = 0;
@@ -1177,6 +1227,10 @@ struct rt_scene {
   int blocks_per_cu[kNumVariants] = {0, 0, 0};
   GNode4* d_nodes4 = nullptr;
   int n_gnodes4 = 0;
+  std::vector<GMat> mesh_mats;  // host copy: the analytic materials are appended after these
+  GPrim* d_prims = nullptr;     // analytic primitives (rt_scene_set_analytic), spheres then planes
+  int n_prims = 0;
+  long long table_bytes = 0;    // device bytes of d_mats + d_prims
 };
 
 namespace {
@@ -1554,6 +1608,8 @@ int rt_scene_upload(const rt_scene_soa* s, const rt_bvh_soa* b, int device, rt_s
   sc->n_gnodes = (int)nodes.size();
   sc->n_tris = nt;
   sc->n_meshes = s->n_meshes;
+  sc->mesh_mats = mats;
+  sc->table_bytes = (long long)(std::max<size_t>(mats.size(), 1) * sizeof(GMat));
   sc->depth = depth;
   sc->stack_words = std::max(std::max(1, depth), stack4);
   sc->n_gnodes4 = (int)nodes4.size();
@@ -1646,6 +1702,7 @@ int launch_render(rt_scene* sc, const rt_render_params* p, void* d_out, rt_stats
   std::memset(&P, 0, sizeof P);
   P.nodes = sc->d_nodes; P.nodes4 = sc->d_nodes4; P.tris = sc->d_tris; P.slot2dev = sc->d_slot2dev; P.shade = sc->d_shade; P.fnorm = sc->d_fnorm;
   P.vnorm = sc->d_vnorm; P.tu = sc->d_tu; P.tv = sc->d_tv; P.texels = sc->d_texels; P.mats = sc->d_mats;
+  P.prims = sc->d_prims; P.n_prims = sc->n_prims;
   LaunchCtx& C = sc->ctx[sc->next_ctx];
   const int ci = sc->next_ctx;
   P.ctr = C.d_ctr;
@@ -1835,12 +1892,77 @@ int rt_last_kernel_ms(rt_scene* sc, float* ms) {
   return RT_OK;
 }
 
+int rt_scene_set_analytic(rt_scene* sc, const rt_sphere* spheres, int n_spheres, const rt_plane* planes,
+                          int n_planes) {
+  if (!sc) return fail(RT_ERR_INVALID, "rt_scene_set_analytic: null scene");
+  if (n_spheres < 0 || n_planes < 0 || (n_spheres > 0 && !spheres) || (n_planes > 0 && !planes))
+    return fail(RT_ERR_INVALID, "rt_scene_set_analytic: bad primitive arrays");
+  const long long n = (long long)n_spheres + n_planes;
+  if (n > (1 << 20)) return fail(RT_ERR_INVALID, "rt_scene_set_analytic: more than 2^20 primitives");
+  std::vector<GMat> mats = sc->mesh_mats;
+  std::vector<GPrim> prims((size_t)n);
+  auto add_mat = [&](const rt_material& m) {
+    GMat G;
+    std::memset(&G, 0, sizeof G);
+    for (int k = 0; k < 3; ++k) {
+      G.ka[k] = m.ambient[k];
+      G.kd[k] = m.diffuse[k];
+      G.ks[k] = m.specular[k];
+    }
+    G.shininess = m.shininess;
+    G.mirror = m.mirror;
+    G.shadowable = m.shadowable;
+    G.draw_mode = RT_DRAW_FLAT;
+    G.tex_w = -1;
+    mats.push_back(G);
+    return (int)mats.size() - 1;
+  };
+  for (int i = 0; i < n_spheres; ++i) {
+    GPrim& G = prims[i];
+    std::memset(&G, 0, sizeof G);
+    for (int k = 0; k < 3; ++k) G.c[k] = spheres[i].center[k];
+    G.r = spheres[i].radius;
+    G.type = kPrimSphere;
+    G.mat = add_mat(spheres[i].material);
+  }
+  for (int i = 0; i < n_planes; ++i) {
+    GPrim& G = prims[(size_t)n_spheres + i];
+    std::memset(&G, 0, sizeof G);
+    for (int k = 0; k < 3; ++k) {
+      G.c[k] = planes[i].center[k];
+      G.n[k] = planes[i].normal[k];
+    }
+    G.type = kPrimPlane;
+    G.mat = add_mat(planes[i].material);
+  }
+  HIP_TRY(hipSetDevice(sc->device));
+  HIP_TRY(hipDeviceSynchronize());   // launches in flight read the old tables
+  long long bytes = 0;
+  GMat* d_mats = nullptr;
+  GPrim* d_prims = nullptr;
+  int rc = upload(&d_mats, mats, bytes);
+  if (rc == RT_OK) rc = upload(&d_prims, prims, bytes);
+  if (rc != RT_OK) {
+    if (d_mats) (void)hipFree(d_mats);
+    if (d_prims) (void)hipFree(d_prims);
+    return rc;
+  }
+  if (sc->d_mats) (void)hipFree(sc->d_mats);
+  if (sc->d_prims) (void)hipFree(sc->d_prims);
+  sc->d_mats = d_mats;
+  sc->d_prims = d_prims;
+  sc->n_prims = (int)n;
+  sc->bytes += bytes - sc->table_bytes;
+  sc->table_bytes = bytes;
+  return RT_OK;
+}
+
 void rt_scene_free(rt_scene* sc) {
   if (!sc) return;
   (void)hipSetDevice(sc->device);
   (void)hipDeviceSynchronize();   // launches may still be reading the scene
   void* ptrs[] = {sc->d_nodes, sc->d_nodes4, sc->d_tris, sc->d_shade, sc->d_fnorm, sc->d_vnorm, sc->d_tu,
-                  sc->d_tv, sc->d_texels, sc->d_mats, sc->d_lights, sc->d_slot2dev};
+                  sc->d_tv, sc->d_texels, sc->d_mats, sc->d_lights, sc->d_slot2dev, sc->d_prims};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   for (LaunchCtx& c : sc->ctx) {

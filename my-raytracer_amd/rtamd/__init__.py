@@ -174,11 +174,24 @@ class HostScene:
 class DeviceScene:
     """Scene resident on one MI355X (rt_scene*), uploaded from a prepared HostScene."""
 
-    def __init__(self, host_scene, device=0):
+    def __init__(self, host_scene, device=0, analytic=False):
+        """analytic=True also uploads the raw scene's spheres and planes (rt_scene_set_analytic,
+        CPU intersect_scene semantics); the default traces meshes only, like the reference GPU
+        path (mytracer_gpu.cu:314-328)."""
         self._h = C.c_void_p()
         self.device = device
         _check_hip(hip_lib().rt_scene_upload(host_scene.soa, host_scene.bvh, device, C.byref(self._h)),
                    "rt_scene_upload")
+        self.analytic = False
+        if analytic:
+            r = host_scene.raw.contents
+            self.set_analytic(r.spheres, r.n_spheres, r.planes, r.n_planes)
+
+    def set_analytic(self, spheres, n_spheres, planes, n_planes):
+        """Replaces the analytic primitives (ctypes arrays/pointers of abi.Sphere / abi.Plane)."""
+        _check_hip(hip_lib().rt_scene_set_analytic(self._h, spheres, n_spheres, planes, n_planes),
+                   "rt_scene_set_analytic")
+        self.analytic = (n_spheres + n_planes) > 0
 
     def close(self):
         if self._h:

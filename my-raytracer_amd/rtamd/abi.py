@@ -115,6 +115,7 @@ class GenParams(C.Structure):
 # Symbols each library must export (declared in include/*.h).
 HIP_SYMBOLS = {
     "rt_scene_upload": (C.c_int, [C.POINTER(SceneSoA), C.POINTER(BvhSoA), C.c_int, C.POINTER(C.c_void_p)]),
+    "rt_scene_set_analytic": (C.c_int, [C.c_void_p, C.POINTER(Sphere), C.c_int, C.POINTER(Plane), C.c_int]),
     "rt_scene_device_bytes": (C.c_longlong, [C.c_void_p]),
     "rt_rows_in_shard": (C.c_int, [C.POINTER(RenderParams)]),
     "rt_launch_compute_image": (C.c_int, [C.c_void_p, C.POINTER(RenderParams), C.c_void_p,

@@ -342,3 +342,107 @@ def test_adaptive_end_to_end_and_full_frame_only():
     p.stripe_count, p.stripe_height = 2, 16
     with pytest.raises(rtamd.RtError):
         dev.render_adaptive(p)
+
+
+# ---- analytic primitives (opt-in: DeviceScene(..., analytic=True)) ----
+SPHERE_MAT = "0.05 0.02 0.02  0.7 0.25 0.2  0.6 0.6 0.6  50  0.0  1"
+CHROME_MAT = "0.02 0.02 0.02  0.2 0.2 0.25  0.8 0.8 0.8  80  0.5  1"
+FLOOR_MAT = "0.1 0.1 0.1  0.45 0.5 0.45  0.1 0.1 0.1  8  0.25  1"
+SKY_MAT = "0.3 0.35 0.4  0.1 0.1 0.2  0.0 0.0 0.0  1  0.0  0"
+
+
+def _mixed_scene(tmp_path, base, enclosed=False):
+    """A KAT mesh scene plus spheres and planes: analytic objects in front of, behind and
+    cutting through triangles, a mirror sphere, a reflective floor plane, a plane through
+    the eye (every primary ray has t = 0 <= 1e-5 there) and optionally an enclosing sphere."""
+    path = kat_scenes.write(tmp_path, base)
+    extra = [
+        f"sphere 0.9 -0.3 0.3  0.45  {SPHERE_MAT}",
+        f"sphere -0.6 0.35 -0.6  0.5  {CHROME_MAT}",
+        f"sphere 0.05 0.1 1.5  0.2  {SPHERE_MAT}",
+        f"plane 0 -1.15 0  0 1 0  {FLOOR_MAT}",
+        f"plane 0 0 -3  0.6 0 0.8  {SPHERE_MAT}",
+        f"plane 0.013 0 0  1 0 0  {SPHERE_MAT}",
+    ]
+    if enclosed:
+        extra.append(f"sphere 0 0 0  12  {SKY_MAT}")
+    with open(path, "a") as f:
+        f.write("\n".join(extra) + "\n")
+    return path
+
+
+def test_analytic_spheres_scene_matches_cpu_oracle():
+    # Config 1 (spheres_proxy, 640x480) on the GPU with CPU intersect_scene semantics.
+    hs = rtamd.HostScene.generate("spheres")
+    hs.prepare()
+    dev = rtamd.DeviceScene(hs, 0, analytic=True)
+    orc = pyoracle.Oracle(hs.raw, hs)
+    for w, h, spp in ((640, 480, 1), (97, 61, 3)):
+        p = hs.render_params(w, h, spp)
+        ref, cnt = orc.render(p, pyoracle.MODE_REFERENCE)
+        p.out_format = rtamd.RT_OUT_RGB_F64
+        img, st = dev.render(p)
+        assert np.abs(img - ref).max() <= TOL64
+        assert counts(st) == [cnt.primary_rays, cnt.shadow_rays, cnt.reflection_rays]
+        assert st.shadow_rays > 0 and st.reflection_rays > 0
+        p.out_format = rtamd.RT_OUT_RGB_F32
+        img32, _ = dev.render(p)
+        assert np.abs(img32.astype(np.float64) - ref).max() <= TOL32
+    # removing them restores the reference GPU path (meshes only => background)
+    dev.set_analytic(None, 0, None, 0)
+    img, st = dev.render(hs.render_params(32, 24, 1))
+    assert np.all(img == np.float32(hs.render_params(32, 24, 1).background[0])) and st.shadow_rays == 0
+
+
+@pytest.mark.parametrize("base,enclosed", [("mirror", False), ("shadow", False), ("phong", True)])
+def test_analytic_mixed_scene_matches_cpu_oracle(tmp_path, base, enclosed):
+    hs = rtamd.HostScene.load(_mixed_scene(tmp_path, base, enclosed))
+    hs.prepare()
+    assert hs.raw.contents.n_spheres >= 3 and hs.raw.contents.n_planes == 3
+    dev = rtamd.DeviceScene(hs, 0, analytic=True)
+    orc = pyoracle.Oracle(hs.raw, hs)
+    for w, h, spp in ((160, 120, 1), (41, 29, 2)):
+        p = hs.render_params(w, h, spp)
+        ref, cnt = orc.render(p, pyoracle.MODE_REFERENCE)
+        p.out_format = rtamd.RT_OUT_RGB_F64
+        img, st = dev.render(p)
+        assert np.abs(img - ref).max() <= TOL64
+        assert counts(st) == [cnt.primary_rays, cnt.shadow_rays, cnt.reflection_rays]
+    # analytic hits bound the BVH window exactly as the oracle's ordered replica does
+    p = hs.render_params(160, 120, 1)
+    p.flags = rtamd.RT_FLAG_TRAVERSAL_STATS
+    _, st = dev.render(p)
+    _, cnt = orc.render(p, pyoracle.MODE_ORDERED)
+    assert (st.node_visits, st.tri_tests, st.closest_hits) == (cnt.node_visits, cnt.tri_tests, cnt.closest_hits)
+
+
+def test_analytic_adaptive_pass_and_stripes():
+    import torch
+
+    hs = rtamd.HostScene.generate("spheres")
+    hs.prepare()
+    dev = rtamd.DeviceScene(hs, 0, analytic=True)
+    orc = pyoracle.Oracle(hs.raw, hs)
+    p = hs.render_params(160, 120, 1)
+    prim, _ = orc.render(p)
+    ref, cnt, sel = orc.adaptive(p, prim, subp=4, threshold=0.02)
+    assert sel.sum() > 0
+    d_prim = torch.from_numpy(prim).cuda()
+    p.out_format = rtamd.RT_OUT_RGB_F64
+    out = torch.zeros((120, 160, 3), dtype=torch.float64, device="cuda")
+    st, nsel = dev.launch_adaptive(p, d_prim.data_ptr(), out.data_ptr(), 4, 0.02, stats=True)
+    assert nsel == int(sel.sum())
+    assert np.abs(out.cpu().numpy() - ref).max() <= TOL64
+    assert counts(st) == [cnt.primary_rays, cnt.shadow_rays, cnt.reflection_rays]
+    full, _ = dev.render(p)
+    p.stripe_height, p.stripe_count, p.stripe_index = 16, 3, 1
+    part, _ = dev.render(p)
+    assert np.array_equal(part, full[rtamd.shard_rows(120, 16, 3, 1)])
+
+
+def test_analytic_bad_arguments_fail_loudly():
+    hs, dev, _ = Case.get("cornell")
+    with pytest.raises(rtamd.RtError):
+        dev.set_analytic(None, 1, None, 0)
+    with pytest.raises(rtamd.RtError):
+        dev.set_analytic(None, 0, None, -1)
