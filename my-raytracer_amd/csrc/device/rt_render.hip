@@ -871,8 +871,8 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
               const TriShade sh = P.shade[best];
               double u = alpha * P.tu[sh.t[0]] + beta * P.tu[sh.t[1]] + gamma * P.tu[sh.t[2]];
               double v = alpha * P.tv[sh.t[0]] + beta * P.tv[sh.t[1]] + gamma * P.tv[sh.t[2]];
-              u = u < 0.0 ? 0.0 : (1.0 < u ? 1.0 : u);
-              v = v < 0.0 ? 0.0 : (1.0 < v ? 1.0 : v);
+              u = fmin(fmax(u, 0.0), 1.0);   // NaN -> 0, as mytracer_gpu.cu:532-533
+              v = fmin(fmax(v, 0.0), 1.0);
               const unsigned TW = (unsigned)Mt.tex_w, TH = (unsigned)Mt.tex_h;
               const int tx = (int)round(u * (TW - 1));
               const int ty = (int)round((1.0 - v) * (TH - 1));

@@ -85,48 +85,24 @@ bool read_ppm(const std::vector<unsigned char>& d, int& w, int& h, std::vector<u
   return true;
 }
 
-// --- PNG (8-bit gray / RGB / RGBA / gray+alpha, not interlaced) ---
+// --- PNG: every standard colour type and bit depth (gray 1/2/4/8/16, RGB 8/16,
+// palette 1/2/4/8, gray+alpha 8/16, RGBA 8/16), plain or Adam7-interlaced.  Converted
+// to RGB8 the way lodepng's RGBA8 decode does (the usual course Image loader): 16-bit
+// samples keep their high byte, low-bit gray scales as v*255/(2^depth-1), palette
+// indices look up PLTE; alpha is dropped (the texel is used as an RGB colour). ---
 uint32_t be32(const unsigned char* p) { return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3]; }
 
-bool read_png(const std::vector<unsigned char>& d, int& w, int& h, std::vector<unsigned char>& rgb) {
-  static const unsigned char sig[8] = {137, 80, 78, 71, 13, 10, 26, 10};
-  if (d.size() < 8 || std::memcmp(d.data(), sig, 8) != 0) return false;
-  size_t pos = 8;
-  int depth = 0, ctype = 0, interlace = 0;
-  std::vector<unsigned char> idat;
-  while (pos + 8 <= d.size()) {
-    const uint32_t len = be32(&d[pos]);
-    const std::string type((const char*)&d[pos + 4], 4);
-    if (pos + 12 + len > d.size()) return false;
-    const unsigned char* body = &d[pos + 8];
-    if (type == "IHDR") {
-      w = (int)be32(body); h = (int)be32(body + 4);
-      depth = body[8]; ctype = body[9]; interlace = body[12];
-    } else if (type == "IDAT") {
-      idat.insert(idat.end(), body, body + len);
-    } else if (type == "IEND") {
-      break;
-    }
-    pos += 12 + len;
-  }
-  if (depth != 8 || interlace != 0 || w <= 0 || h <= 0) return false;
-  int ch;
-  switch (ctype) { case 0: ch = 1; break; case 2: ch = 3; break; case 4: ch = 2; break; case 6: ch = 4; break; default: return false; }
-  const size_t stride = (size_t)w * ch;
-  std::vector<unsigned char> raw((stride + 1) * h);
-  uLongf raw_len = raw.size();
-  if (uncompress(raw.data(), &raw_len, idat.data(), idat.size()) != Z_OK || raw_len != raw.size()) return false;
-  std::vector<unsigned char> img(stride * h);
-  for (int y = 0; y < h; ++y) {
-    const unsigned char filter = raw[y * (stride + 1)];
-    const unsigned char* src = &raw[y * (stride + 1) + 1];
-    unsigned char* dst = &img[y * stride];
-    const unsigned char* prev = y > 0 ? &img[(y - 1) * stride] : nullptr;
+bool png_unfilter(const unsigned char* src, unsigned char* dst, size_t stride, int rows, int bpp) {
+  for (int y = 0; y < rows; ++y) {
+    const unsigned char filter = src[y * (stride + 1)];
+    const unsigned char* in = &src[y * (stride + 1) + 1];
+    unsigned char* out = &dst[y * stride];
+    const unsigned char* prev = y > 0 ? &dst[(y - 1) * stride] : nullptr;
     for (size_t x = 0; x < stride; ++x) {
-      const int a = x >= (size_t)ch ? dst[x - ch] : 0;
+      const int a = x >= (size_t)bpp ? out[x - bpp] : 0;
       const int b = prev ? prev[x] : 0;
-      const int c = (prev && x >= (size_t)ch) ? prev[x - ch] : 0;
-      int v = src[x];
+      const int c = (prev && x >= (size_t)bpp) ? prev[x - bpp] : 0;
+      int v = in[x];
       switch (filter) {
         case 0: break;
         case 1: v += a; break;
@@ -136,12 +112,97 @@ bool read_png(const std::vector<unsigned char>& d, int& w, int& h, std::vector<u
                   v += (pa <= pb && pa <= pc) ? a : (pb <= pc ? b : c); break; }
         default: return false;
       }
-      dst[x] = (unsigned char)v;
+      out[x] = (unsigned char)v;
     }
   }
-  rgb.resize(3 * (size_t)w * h);
-  for (size_t i = 0; i < (size_t)w * h; ++i) {
-    for (int k = 0; k < 3; ++k) rgb[3 * i + k] = (ch >= 3) ? img[i * ch + k] : img[i * ch];
+  return true;
+}
+
+bool read_png(const std::vector<unsigned char>& d, int& w, int& h, std::vector<unsigned char>& rgb) {
+  static const unsigned char sig[8] = {137, 80, 78, 71, 13, 10, 26, 10};
+  if (d.size() < 8 || std::memcmp(d.data(), sig, 8) != 0) return false;
+  size_t pos = 8;
+  int depth = 0, ctype = -1, interlace = 0;
+  bool have_ihdr = false;
+  std::vector<unsigned char> idat, plte;
+  while (pos + 8 <= d.size()) {
+    const uint32_t len = be32(&d[pos]);
+    const std::string type((const char*)&d[pos + 4], 4);
+    if (len > d.size() || pos + 12 + len > d.size()) return false;
+    const unsigned char* body = &d[pos + 8];
+    if (type == "IHDR") {
+      if (len < 13) return false;
+      w = (int)be32(body); h = (int)be32(body + 4);
+      depth = body[8]; ctype = body[9]; interlace = body[12];
+      have_ihdr = true;
+    } else if (type == "PLTE") {
+      plte.assign(body, body + len);
+    } else if (type == "IDAT") {
+      idat.insert(idat.end(), body, body + len);
+    } else if (type == "IEND") {
+      break;
+    }
+    pos += 12 + len;
+  }
+  if (!have_ihdr || w <= 0 || h <= 0 || (long long)w * h > (1ll << 28) || interlace > 1) return false;
+  int ch;
+  switch (ctype) { case 0: ch = 1; break; case 2: ch = 3; break; case 3: ch = 1; break; case 4: ch = 2; break;
+                   case 6: ch = 4; break; default: return false; }
+  const bool depth_ok = ctype == 0 ? (depth == 1 || depth == 2 || depth == 4 || depth == 8 || depth == 16)
+                      : ctype == 3 ? (depth == 1 || depth == 2 || depth == 4 || depth == 8)
+                                   : (depth == 8 || depth == 16);
+  if (!depth_ok || (ctype == 3 && (plte.empty() || plte.size() % 3 != 0))) return false;
+  const int bits_pp = ch * depth;
+  const int bpp = std::max(1, bits_pp / 8);
+  // passes: Adam7 (7 sub-images) or one full image
+  static const int IX[7] = {0, 4, 0, 2, 0, 1, 0}, IY[7] = {0, 0, 4, 0, 2, 0, 1};
+  static const int DX[7] = {8, 8, 4, 4, 2, 2, 1}, DY[7] = {8, 8, 8, 4, 4, 2, 2};
+  const int npass = interlace ? 7 : 1;
+  int pw[7], ph[7];
+  size_t raw_size = 0;
+  for (int p = 0; p < npass; ++p) {
+    pw[p] = interlace ? (w > IX[p] ? (w - IX[p] + DX[p] - 1) / DX[p] : 0) : w;
+    ph[p] = interlace ? (h > IY[p] ? (h - IY[p] + DY[p] - 1) / DY[p] : 0) : h;
+    if (pw[p] > 0 && ph[p] > 0) raw_size += (size_t)ph[p] * (1 + ((size_t)pw[p] * bits_pp + 7) / 8);
+  }
+  std::vector<unsigned char> raw(raw_size);
+  uLongf raw_len = raw.size();
+  if (uncompress(raw.data(), &raw_len, idat.data(), idat.size()) != Z_OK || raw_len != raw.size()) return false;
+  const int maxv = (1 << depth) - 1;
+  auto sample = [&](const unsigned char* line, int x, int c) -> int {
+    if (depth == 8) return line[(size_t)x * ch + c];
+    if (depth == 16) return line[2 * ((size_t)x * ch + c)];   // high byte
+    const size_t bit = (size_t)x * depth;                      // ch == 1 for depth < 8
+    return (line[bit / 8] >> (8 - depth - (int)(bit % 8))) & maxv;
+  };
+  rgb.assign(3 * (size_t)w * h, 0);
+  size_t off = 0;
+  std::vector<unsigned char> img;
+  for (int p = 0; p < npass; ++p) {
+    if (pw[p] == 0 || ph[p] == 0) continue;
+    const size_t stride = ((size_t)pw[p] * bits_pp + 7) / 8;
+    img.assign(stride * ph[p], 0);
+    if (!png_unfilter(&raw[off], img.data(), stride, ph[p], bpp)) return false;
+    off += (stride + 1) * ph[p];
+    for (int y = 0; y < ph[p]; ++y) {
+      const unsigned char* line = &img[y * stride];
+      const int oy = interlace ? IY[p] + y * DY[p] : y;
+      for (int x = 0; x < pw[p]; ++x) {
+        const int ox = interlace ? IX[p] + x * DX[p] : x;
+        unsigned char* o = &rgb[3 * ((size_t)oy * w + ox)];
+        if (ctype == 3) {
+          const int idx = sample(line, x, 0);
+          if (3 * (size_t)idx + 2 >= plte.size()) return false;
+          for (int k = 0; k < 3; ++k) o[k] = plte[3 * idx + k];
+        } else if (ch >= 3) {
+          for (int k = 0; k < 3; ++k) o[k] = (unsigned char)sample(line, x, k);
+        } else {
+          const int g = sample(line, x, 0);
+          const unsigned char v = depth < 8 ? (unsigned char)(g * 255 / maxv) : (unsigned char)g;
+          o[0] = o[1] = o[2] = v;
+        }
+      }
+    }
   }
   return true;
 }
@@ -166,7 +227,11 @@ std::map<std::string, std::string> read_mtl(const std::string& path) {
     std::string key;
     if (!(ls >> key)) continue;
     if (key == "newmtl") ls >> cur;
-    else if (key == "map_Kd") { std::string fn; ls >> fn; tex[cur] = dir_of(path) + fn; }
+    else if (key == "map_Kd") {   // options (-s u v w, -bm b, ...) precede the file name: take the last token
+      std::string fn, t;
+      while (ls >> t) fn = t;
+      if (!fn.empty()) tex[cur] = dir_of(path) + fn;
+    }
   }
   return tex;
 }

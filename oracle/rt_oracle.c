@@ -503,8 +503,8 @@ static void triangle_shade(const or_ctx* C, tri_ref tr, const ray_t* r, double t
     const int* iuv = M->tri_uv + 3 * tr.tri;
     double u = alpha * M->u[iuv[0]] + beta * M->u[iuv[1]] + gamma * M->u[iuv[2]];
     double v = alpha * M->v[iuv[0]] + beta * M->v[iuv[1]] + gamma * M->v[iuv[2]];
-    u = u < 0.0 ? 0.0 : (1.0 < u ? 1.0 : u);
-    v = v < 0.0 ? 0.0 : (1.0 < v ? 1.0 : v);
+    u = fmin(fmax(u, 0.0), 1.0);   /* NaN -> 0, as mytracer_gpu.cu:532-533 */
+    v = fmin(fmax(v, 0.0), 1.0);
     const unsigned W = (unsigned)M->texture.width, H = (unsigned)M->texture.height;
     const int px = (int)round(u * (W - 1));
     const int py = (int)round((1.0 - v) * (H - 1));
