@@ -63,6 +63,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="cpu_baseline: minimum timed CPU work")
     ap.add_argument("--save", default="", help="rank 0: save the gathered image (.npy)")
     ap.add_argument("--streams", type=int, default=4, help="frames in flight (1 = strictly serial frames)")
+    ap.add_argument("--tree", choices=["sah", "reference"], default="sah",
+                    help="device traversal hierarchy (pixels identical either way; DESIGN.md §4)")
     ap.add_argument("--analytic", action="store_true",
                     help="also trace the scene's spheres/planes (always on for --scene spheres)")
     ap.add_argument("--adaptive", action="store_true",
@@ -90,7 +92,8 @@ def main():
     gen = {"n_triangles": a.tris} if a.scene == "random_tris" and a.tris else {}
     host = rtamd.HostScene.generate(a.scene, **gen)
     build_s = host.prepare()
-    gpu = rtamd.DeviceScene(host, device=local, analytic=a.analytic or a.scene == "spheres")
+    gpu = rtamd.DeviceScene(host, device=local, analytic=a.analytic or a.scene == "spheres",
+                             tree=a.tree)
     params = host.render_params(a.width, a.height, a.spp)
     params.stripe_height = STRIPE_H
     params.stripe_count = n
@@ -196,7 +199,8 @@ def main():
                 "workload": f"{a.scene}_proxy {a.width}x{a.height} spp={a.spp * a.spp} depth={params.max_depth} "
                             f"lights={params.n_lights}",
                 "triangles": host.triangle_count,
-                "bvh": f"reference median split, depth {host.bvh_depth}",
+                "bvh": f"host: reference median split, depth {host.bvh_depth}; device: "
+                       + ("binned-SAH hierarchy, 4-wide" if a.tree == "sah" else "reference tree refined, 4-wide"),
                 "rays_per_frame": int(rays_total),
                 "rays_breakdown_rank0": {"primary": st.primary_rays, "shadow": st.shadow_rays,
                                          "reflection": st.reflection_rays},

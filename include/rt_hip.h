@@ -142,6 +142,22 @@ typedef struct rt_scene rt_scene;   /* opaque device-resident scene */
  * host SoA + reference BVH into the MI355X layout.  Leaves the device current. */
 int rt_scene_upload(const rt_scene_soa* soa, const rt_bvh_soa* bvh, int device, rt_scene** out);
 
+/* Device traversal hierarchy (never changes a pixel or a ray count: the closest hit is
+ * the smallest (t, reference slot) over a conservative superset of candidates, DESIGN.md
+ * §4; the canonical counters always walk the reference tree given in `bvh`).
+ *   RT_TREE_SAH        binned-SAH tree over all triangles, 4-wide collapsed (default)
+ *   RT_TREE_REFERENCE  the reference median-split tree, oversize leaves refined */
+enum { RT_TREE_SAH = 0, RT_TREE_REFERENCE = 1 };
+typedef struct rt_upload_options {
+  int device_tree;      /* RT_TREE_* */
+  int reserved_[7];
+} rt_upload_options;
+
+/* rt_scene_upload with options (NULL = defaults; the environment variable
+ * RT_DEVICE_TREE=reference|sah changes the default for A/B runs). */
+int rt_scene_upload_ex(const rt_scene_soa* soa, const rt_bvh_soa* bvh, int device, const rt_upload_options* opt,
+                       rt_scene** out);
+
 /* Device bytes held by the scene (nodes, triangles, shading data). */
 long long rt_scene_device_bytes(const rt_scene* scene);
 

@@ -35,6 +35,10 @@
 #include <cstring>
 #include <string>
 #include <vector>
+#include <atomic>
+#include <climits>
+#include <thread>
+#include <chrono>
 
 #include "../../../include/rt_hip.h"
 #include "rt_layout.hpp"
@@ -1255,6 +1259,12 @@ struct DevTree {
   std::vector<std::array<double, 3>> lo, hi;
   std::vector<int> left, right;    // internal: children (device-tree ids)
   std::vector<int> first, count;   // count > 0: leaf of device records [first, first + count)
+  void reserve(size_t n) {
+    lo.reserve(n); hi.reserve(n); left.reserve(n); right.reserve(n); first.reserve(n); count.reserve(n);
+  }
+  void resize(size_t n) {
+    lo.resize(n); hi.resize(n); left.resize(n, -1); right.resize(n, -1); first.resize(n, 0); count.resize(n, 0);
+  }
   int add() {
     lo.push_back({0, 0, 0});
     hi.push_back({0, 0, 0});
@@ -1268,6 +1278,7 @@ struct DevTree {
 
 void build_device_tree(const rt_scene_soa* s, const rt_bvh_soa* b, DevTree& E, std::vector<uint32_t>& dev2slot) {
   const long long nt = s->n_vertex_idx / 3;
+  E.reserve(2 * (size_t)nt);
   for (long long i = 0; i < nt; ++i) dev2slot[i] = (uint32_t)i;
   auto vtx = [&](uint32_t slot, int c) { return s->vertex_pos + 3 * (size_t)s->vertex_idx[3 * (size_t)slot + c]; };
   auto centroid = [&](uint32_t slot, int k) { return (vtx(slot, 0)[k] + vtx(slot, 1)[k] + vtx(slot, 2)[k]) / 3.0; };
@@ -1336,6 +1347,262 @@ void build_device_tree(const rt_scene_soa* s, const rt_bvh_soa* b, DevTree& E, s
   }
 }
 
+// Device hierarchy option "sah": a binned-SAH tree over all triangles, split down to
+// kLeafMax per leaf, instead of the reference tree + refinement.  Pixels do not depend
+// on it (smallest (t, slot) over a conservative superset); the canonical
+// 2-wide kernel keeps walking the reference tree through slot2dev.  Parallel: the top
+// splits bin on all threads, the subtrees below them are built on threads into local
+// arenas and appended in job order, so the tree does not depend on the thread count.
+int sah_threads() {
+  const char* e = std::getenv("RT_BUILD_THREADS");
+  int t = e ? std::atoi(e) : 0;
+  if (t <= 0) {
+    const char* o = std::getenv("OMP_NUM_THREADS");
+    t = o ? std::atoi(o) : 0;
+  }
+  if (t <= 0) t = (int)std::thread::hardware_concurrency();
+  return std::max(1, std::min(t, 64));
+}
+
+struct SahData {
+  std::vector<std::array<double, 3>> lo, hi, c;   // per reference slot: bounds, centroid
+};
+using V3 = std::array<double, 3>;
+constexpr int kSahBins = 32;
+const V3 kV3Lo = {DBL_MAX, DBL_MAX, DBL_MAX}, kV3Hi = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
+
+inline void grow3(V3& lo, V3& hi, const V3& l2, const V3& h2) {
+  for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], l2[k]); hi[k] = std::max(hi[k], h2[k]); }
+}
+inline double half_area(const V3& lo, const V3& hi) {
+  const double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+  return dx * dy + dy * dz + dz * dx;
+}
+
+// Splits records [first, first + count) of idx (partitioned in place): fills the node box,
+// returns the split position, or -1 for a leaf.  `threads` > 1 bins in parallel chunks.
+long long sah_split(const SahData& D, std::vector<uint32_t>& idx, long long first, long long count, V3& lo, V3& hi,
+                    int threads) {
+  struct Part { V3 lo, hi, clo, chi; };
+  struct Bins { V3 lo[3][kSahBins], hi[3][kSahBins]; long long n[3][kSahBins]; };
+  const int T = (threads > 1 && count >= (1 << 16)) ? threads : 1;
+  auto chunk = [&](int t, long long& a, long long& b) { a = first + count * t / T; b = first + count * (t + 1) / T; };
+  Part parts_local[1];
+  std::vector<Part> parts_vec(T > 1 ? T : 0);
+  Part* parts = T > 1 ? parts_vec.data() : parts_local;
+  auto run = [&](auto&& fn) {
+    if (T == 1) { fn(0); return; }
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t) th.emplace_back(fn, t);
+    for (auto& x : th) x.join();
+  };
+  run([&](int t) {
+    long long a, b;
+    chunk(t, a, b);
+    Part P{kV3Lo, kV3Hi, kV3Lo, kV3Hi};
+    for (long long r = a; r < b; ++r) {
+      const uint32_t q = idx[r];
+      grow3(P.lo, P.hi, D.lo[q], D.hi[q]);
+      grow3(P.clo, P.chi, D.c[q], D.c[q]);
+    }
+    parts[t] = P;
+  });
+  V3 clo = kV3Lo, chi = kV3Hi;
+  lo = kV3Lo; hi = kV3Hi;
+  for (int t = 0; t < T; ++t) { grow3(lo, hi, parts[t].lo, parts[t].hi); grow3(clo, chi, parts[t].clo, parts[t].chi); }
+  if (count <= kLeafMax) return -1;
+  if (count <= 4) {   // tiny node: object median on the longest centroid axis
+    int axis = 0;
+    for (int k = 1; k < 3; ++k)
+      if (chi[k] - clo[k] > chi[axis] - clo[axis]) axis = k;
+    const long long mid = first + count / 2;
+    std::nth_element(idx.begin() + first, idx.begin() + mid, idx.begin() + first + count,
+                     [&](uint32_t a, uint32_t b) { return D.c[a][axis] < D.c[b][axis] || (D.c[a][axis] == D.c[b][axis] && a < b); });
+    return mid;
+  }
+  const int nb = (int)std::min<long long>(kSahBins, count);   // bins in use
+  double scale[3];
+  for (int k = 0; k < 3; ++k) scale[k] = chi[k] > clo[k] ? nb / (chi[k] - clo[k]) : 0.0;
+  auto bin_of = [&](uint32_t q, int k) { return std::min(nb - 1, (int)((D.c[q][k] - clo[k]) * scale[k])); };
+  Bins local;
+  std::vector<Bins> extra(T > 1 ? T - 1 : 0);
+  auto bins_of = [&](int t) -> Bins& { return t == 0 ? local : extra[t - 1]; };
+  run([&](int t) {
+    Bins& B = bins_of(t);
+    for (int k = 0; k < 3; ++k)
+      for (int i = 0; i < nb; ++i) { B.lo[k][i] = kV3Lo; B.hi[k][i] = kV3Hi; B.n[k][i] = 0; }
+    long long a, b;
+    chunk(t, a, b);
+    for (long long r = a; r < b; ++r) {
+      const uint32_t q = idx[r];
+      for (int k = 0; k < 3; ++k) {
+        if (scale[k] == 0.0) continue;
+        const int bi = bin_of(q, k);
+        grow3(B.lo[k][bi], B.hi[k][bi], D.lo[q], D.hi[q]);
+        B.n[k][bi]++;
+      }
+    }
+  });
+  for (int t = 1; t < T; ++t)
+    for (int k = 0; k < 3; ++k)
+      for (int i = 0; i < nb; ++i) {
+        grow3(local.lo[k][i], local.hi[k][i], extra[t - 1].lo[k][i], extra[t - 1].hi[k][i]);
+        local.n[k][i] += extra[t - 1].n[k][i];
+      }
+  const Bins& B = local;
+  double best_cost = DBL_MAX;
+  int best_axis = -1, best_split = 0;
+  for (int k = 0; k < 3; ++k) {
+    if (scale[k] == 0.0) continue;
+    double right_cost[kSahBins];
+    V3 rlo = kV3Lo, rhi = kV3Hi;
+    long long rn = 0;
+    for (int i = nb - 1; i > 0; --i) {
+      grow3(rlo, rhi, B.lo[k][i], B.hi[k][i]);
+      rn += B.n[k][i];
+      right_cost[i] = rn ? half_area(rlo, rhi) * (double)rn : 0.0;
+    }
+    V3 llo = kV3Lo, lhi = kV3Hi;
+    long long ln = 0;
+    for (int i = 0; i < nb - 1; ++i) {
+      grow3(llo, lhi, B.lo[k][i], B.hi[k][i]);
+      ln += B.n[k][i];
+      if (ln == 0 || ln == count) continue;
+      const double cost = half_area(llo, lhi) * (double)ln + right_cost[i + 1];
+      if (cost < best_cost) { best_cost = cost; best_axis = k; best_split = i + 1; }
+    }
+  }
+  if (best_axis < 0) return first + count / 2;   // all centroids equal: halve in slot order
+  return std::partition(idx.begin() + first, idx.begin() + first + count,
+                        [&](uint32_t q) { return bin_of(q, best_axis) < best_split; }) - idx.begin();
+}
+
+// Builds the subtree of records [first, first + count) under node `root` of T.
+void sah_subtree(const SahData& D, std::vector<uint32_t>& idx, DevTree& T, int root, long long first, long long count) {
+  struct Job { int id; long long first, count; };
+  std::vector<Job> jobs = {{root, first, count}};
+  while (!jobs.empty()) {
+    const Job j = jobs.back();
+    jobs.pop_back();
+    V3 lo, hi;
+    const long long mid = sah_split(D, idx, j.first, j.count, lo, hi, 1);
+    T.lo[j.id] = lo;
+    T.hi[j.id] = hi;
+    if (mid < 0) {
+      T.first[j.id] = (int)j.first;
+      T.count[j.id] = (int)j.count;
+      continue;
+    }
+    const int l = T.add(), r = T.add();
+    T.left[j.id] = l;
+    T.right[j.id] = r;
+    jobs.push_back({r, mid, j.first + j.count - mid});
+    jobs.push_back({l, j.first, mid - j.first});
+  }
+}
+
+void build_sah_tree(const rt_scene_soa* s, DevTree& E, std::vector<uint32_t>& dev2slot) {
+  const bool timing = std::getenv("RT_UPLOAD_TIMING") != nullptr;
+  auto t_last = std::chrono::steady_clock::now();
+  auto tick = [&](const char* phase) {
+    if (!timing) return;
+    const auto t = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "  sah: %-14s %8.3f s\n", phase, std::chrono::duration<double>(t - t_last).count());
+    t_last = t;
+  };
+  const long long nt = s->n_vertex_idx / 3;
+  const int threads = nt >= 200000 ? sah_threads() : 1;
+  E.reserve(2 * (size_t)nt);
+  SahData D;
+  D.lo.resize((size_t)nt); D.hi.resize((size_t)nt); D.c.resize((size_t)nt);
+  auto prep = [&](long long a, long long b) {
+    for (long long i = a; i < b; ++i) {
+      dev2slot[i] = (uint32_t)i;
+      for (int k = 0; k < 3; ++k) {
+        double lo = DBL_MAX, hi = -DBL_MAX, sum = 0.0;
+        for (int c = 0; c < 3; ++c) {
+          const double v = s->vertex_pos[3 * (size_t)s->vertex_idx[3 * i + c] + k];
+          lo = std::min(lo, v); hi = std::max(hi, v); sum += v;
+        }
+        D.lo[i][k] = lo; D.hi[i][k] = hi; D.c[i][k] = sum / 3.0;
+      }
+    }
+  };
+  {
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; ++t) th.emplace_back(prep, nt * t / threads, nt * (t + 1) / threads);
+    for (auto& x : th) x.join();
+  }
+  tick("prep");
+  // top levels: big jobs split with parallel binning, breadth first
+  struct Job { int id; long long first, count; };
+  const long long kBig = threads > 1 ? std::max<long long>(1 << 15, nt / (8LL * threads)) : LLONG_MAX;
+  std::vector<Job> pending, queue = {{E.add(), 0, nt}};
+  for (size_t q = 0; q < queue.size(); ++q) {
+    const Job j = queue[q];
+    if (j.count < kBig) { pending.push_back(j); continue; }
+    V3 lo, hi;
+    const long long mid = sah_split(D, dev2slot, j.first, j.count, lo, hi, threads);
+    E.lo[j.id] = lo;
+    E.hi[j.id] = hi;
+    if (mid < 0) { E.first[j.id] = (int)j.first; E.count[j.id] = (int)j.count; continue; }
+    const int l = E.add(), r = E.add();
+    E.left[j.id] = l;
+    E.right[j.id] = r;
+    queue.push_back({l, j.first, mid - j.first});
+    queue.push_back({r, mid, j.first + j.count - mid});
+  }
+  tick("top");
+  // subtrees on threads, each into its own arena (local node 0 = the pending node)
+  std::vector<DevTree> arena(pending.size());
+  std::atomic<size_t> next{0};
+  auto worker = [&]() {
+    for (size_t k; (k = next.fetch_add(1)) < pending.size();) {
+      arena[k].add();
+      sah_subtree(D, dev2slot, arena[k], 0, pending[k].first, pending[k].count);
+    }
+  };
+  {
+    std::vector<std::thread> th;
+    for (int t = 0; t < std::min<int>(threads, (int)pending.size()); ++t) th.emplace_back(worker);
+    if (th.empty()) worker();
+    for (auto& x : th) x.join();
+  }
+  tick("subtrees");
+  // append in job order (thread-count independent): arena k's node i > 0 -> base[k] + i
+  std::vector<long long> base(pending.size());
+  long long total = (long long)E.left.size();
+  for (size_t k = 0; k < pending.size(); ++k) {
+    base[k] = total - 1;
+    total += (long long)arena[k].left.size() - 1;
+  }
+  E.resize((size_t)total);
+  next = 0;
+  auto merge = [&]() {
+    for (size_t k; (k = next.fetch_add(1)) < pending.size();) {
+      DevTree& A = arena[k];
+      auto map = [&](int i) { return i == 0 ? pending[k].id : (int)(base[k] + i); };
+      for (size_t i = 0; i < A.left.size(); ++i) {
+        const int id = map((int)i);
+        E.lo[id] = A.lo[i];
+        E.hi[id] = A.hi[i];
+        E.first[id] = A.first[i];
+        E.count[id] = A.count[i];
+        E.left[id] = A.count[i] > 0 ? -1 : map(A.left[i]);
+        E.right[id] = A.count[i] > 0 ? -1 : map(A.right[i]);
+      }
+      A = DevTree();   // free as we go
+    }
+  };
+  {
+    std::vector<std::thread> th;
+    for (int t = 0; t < std::min<int>(threads, (int)pending.size()); ++t) th.emplace_back(merge);
+    if (th.empty()) merge();
+    for (auto& x : th) x.join();
+  }
+  tick("merge");
+}
+
 int validate(const rt_scene_soa* s, const rt_bvh_soa* b) {
   if (!s || !b) return fail(RT_ERR_INVALID, "rt_scene_upload: null scene or bvh");
   if (s->n_vertex_idx % 3 != 0 || s->n_vertex_idx < 0 || s->n_vertices < 0 || s->n_meshes < 0)
@@ -1381,10 +1648,30 @@ const char* rt_build_info(void) {
 }
 
 int rt_scene_upload(const rt_scene_soa* s, const rt_bvh_soa* b, int device, rt_scene** out) {
+  return rt_scene_upload_ex(s, b, device, nullptr, out);
+}
+
+int rt_scene_upload_ex(const rt_scene_soa* s, const rt_bvh_soa* b, int device, const rt_upload_options* opt,
+                       rt_scene** out) {
   if (!out) return fail(RT_ERR_INVALID, "rt_scene_upload: null out");
   *out = nullptr;
+  int tree_kind = RT_TREE_SAH;
+  if (const char* e = std::getenv("RT_DEVICE_TREE"))   // process default override (A/B runs)
+    tree_kind = std::strcmp(e, "reference") == 0 || std::strcmp(e, "median") == 0 ? RT_TREE_REFERENCE : RT_TREE_SAH;
+  if (opt) tree_kind = opt->device_tree;
+  if (tree_kind != RT_TREE_SAH && tree_kind != RT_TREE_REFERENCE)
+    return fail(RT_ERR_INVALID, "rt_scene_upload: unknown device_tree");
+  const bool timing = std::getenv("RT_UPLOAD_TIMING") != nullptr;   // phase times to stderr (diagnostics)
+  auto t_last = std::chrono::steady_clock::now();
+  auto tick = [&](const char* phase) {
+    if (!timing) return;
+    const auto t = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "rt_scene_upload: %-14s %8.3f s\n", phase, std::chrono::duration<double>(t - t_last).count());
+    t_last = t;
+  };
   int rc = validate(s, b);
   if (rc != RT_OK) return rc;
+  tick("validate");
   const long long nt = s->n_vertex_idx / 3;
 
   // ---- delta: conservative growth of the fp32 boxes ----
@@ -1442,6 +1729,7 @@ int rt_scene_upload(const rt_scene_soa* s, const rt_bvh_soa* b, int device, rt_s
       }
     }
   }
+  tick("nodes2");
   // ---- device binary tree: the reference tree with oversize leaves refined ----
   // Reference leaves of more than kLeafMax triangles (coplanar grids the fixed-axis
   // median split cannot separate, mybvh.cpp:95-130) get a sub-tree split on the
@@ -1450,7 +1738,11 @@ int rt_scene_upload(const rt_scene_soa* s, const rt_bvh_soa* b, int device, rt_s
   // of the triangles the ray can hit, so it does not depend on the tree.
   DevTree E;
   std::vector<uint32_t> dev2slot((size_t)std::max<long long>(nt, 1));
-  if (nt > 0) build_device_tree(s, b, E, dev2slot);
+  if (nt > 0) {
+    if (tree_kind == RT_TREE_SAH) build_sah_tree(s, E, dev2slot);
+    else build_device_tree(s, b, E, dev2slot);
+  }
+  tick("device tree");
   std::vector<uint32_t> slot2dev((size_t)std::max<long long>(nt, 1), 0);
   for (long long g = 0; g < nt; ++g) slot2dev[dev2slot[g]] = (uint32_t)g;
 
@@ -1463,17 +1755,20 @@ int rt_scene_upload(const rt_scene_soa* s, const rt_bvh_soa* b, int device, rt_s
       return dx * dy + dy * dz + dz * dx;
     };
     auto internal = [&](int c) { return E.count[c] == 0; };
+    struct Kids { int c[4]; int n; };
     auto kids_of = [&](int n) {   // open the largest internal child until 4 children
-      std::vector<int> k = {E.left[n], E.right[n]};
-      while (k.size() < 4) {
+      Kids k{{E.left[n], E.right[n], -1, -1}, 2};
+      while (k.n < 4) {
         int pick = -1;
         double best_a = -1.0;
-        for (size_t i = 0; i < k.size(); ++i)
-          if (internal(k[i]) && area(k[i]) > best_a) { best_a = area(k[i]); pick = (int)i; }
+        for (int i = 0; i < k.n; ++i)
+          if (internal(k.c[i]) && area(k.c[i]) > best_a) { best_a = area(k.c[i]); pick = i; }
         if (pick < 0) break;
-        const int c = k[pick];
-        k[pick] = E.left[c];
-        k.insert(k.begin() + pick + 1, E.right[c]);
+        const int c = k.c[pick];
+        for (int i = k.n; i > pick + 1; --i) k.c[i] = k.c[i - 1];
+        k.c[pick] = E.left[c];
+        k.c[pick + 1] = E.right[c];
+        k.n++;
       }
       return k;
     };
@@ -1494,7 +1789,7 @@ int rt_scene_upload(const rt_scene_soa* s, const rt_bvh_soa* b, int device, rt_s
       nodes4.push_back(g);
     } else {
       std::vector<int> order;                  // device-tree ids of the collapsed nodes, preorder
-      std::vector<std::vector<int>> kids;
+      std::vector<Kids> kids;
       std::vector<int> g4(E.left.size(), -1);
       std::vector<int> stk = {0};
       while (!stk.empty()) {
@@ -1503,20 +1798,20 @@ int rt_scene_upload(const rt_scene_soa* s, const rt_bvh_soa* b, int device, rt_s
         g4[n] = (int)order.size();
         order.push_back(n);
         kids.push_back(kids_of(n));
-        const std::vector<int>& k = kids.back();
-        for (int i = (int)k.size() - 1; i >= 0; --i)
-          if (internal(k[i])) stk.push_back(k[i]);
+        const Kids& k = kids.back();
+        for (int i = k.n - 1; i >= 0; --i)
+          if (internal(k.c[i])) stk.push_back(k.c[i]);
       }
       nodes4.resize(order.size());
       std::vector<int> need(order.size(), 0);   // stack entries needed below each node
       for (int gi = (int)order.size() - 1; gi >= 0; --gi) {
         GNode4& g = nodes4[gi];
         std::memset(&g, 0, sizeof g);
-        const std::vector<int>& k = kids[gi];
+        const Kids& k = kids[gi];
         int deeper = 0;
         for (int s_ = 0; s_ < 4; ++s_) {
-          if (s_ < (int)k.size()) {
-            const int c = k[s_];
+          if (s_ < k.n) {
+            const int c = k.c[s_];
             set4(g, s_, c);
             g.ref[s_] = internal(c) ? (uint32_t)g4[c] : (kLeaf | (uint32_t)E.first[c]);
             if (internal(c)) deeper = std::max(deeper, need[g4[c]]);
@@ -1524,12 +1819,13 @@ int rt_scene_upload(const rt_scene_soa* s, const rt_bvh_soa* b, int device, rt_s
             g.ref[s_] = kEmpty;
           }
         }
-        need[gi] = (int)k.size() - 1 + deeper;
+        need[gi] = k.n - 1 + deeper;
       }
       stack4 = std::max(1, need[0]);
     }
   }
 
+  tick("collapse4");
   if (depth > kMaxDepth || stack4 > kMaxDepth)
     return fail(RT_ERR_UNSUPPORTED, "rt_scene_upload: BVH needs more than 4096 traversal-stack entries");
 
@@ -1540,7 +1836,9 @@ int rt_scene_upload(const rt_scene_soa* s, const rt_bvh_soa* b, int device, rt_s
   std::vector<GTri> tris((size_t)nt);
   std::vector<TriShade> shade((size_t)nt);
   std::vector<double> fnorm(3 * (size_t)nt);
-  for (long long g = 0; g < nt; ++g) {
+  std::atomic<bool> bad_uv{false};
+  auto fill = [&](long long g0, long long g1) {
+  for (long long g = g0; g < g1; ++g) {
     const long long i = dev2slot[g];   // reference slot
     const int v0 = s->vertex_idx[3 * i], v1 = s->vertex_idx[3 * i + 1], v2 = s->vertex_idx[3 * i + 2];
     const double* p0 = s->vertex_pos + 3 * (size_t)v0;
@@ -1561,9 +1859,19 @@ int rt_scene_upload(const rt_scene_soa* s, const rt_bvh_soa* b, int device, rt_s
     if (s->mesh_tex_width[T.mesh] > 0)
       for (int k = 0; k < 3; ++k)
         if (sh.t[k] < 0 || sh.t[k] >= s->n_tex_coords)
-          return fail(RT_ERR_INVALID, "rt_scene_upload: textured mesh with invalid uv index");
+          bad_uv = true;
     for (int k = 0; k < 3; ++k) fnorm[3 * (size_t)g + k] = s->face_normals[3 * i + k];
   }
+  };
+  {
+    const int T = nt >= 200000 ? sah_threads() : 1;
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; ++t) th.emplace_back(fill, nt * t / T, nt * (t + 1) / T);
+    fill(0, nt / T);
+    for (auto& x : th) x.join();
+  }
+  if (bad_uv) return fail(RT_ERR_INVALID, "rt_scene_upload: textured mesh with invalid uv index");
+  tick("records");
   std::vector<GMat> mats((size_t)s->n_meshes);
   for (int m = 0; m < s->n_meshes; ++m) {
     GMat& G = mats[m];
@@ -1585,6 +1893,7 @@ int rt_scene_upload(const rt_scene_soa* s, const rt_bvh_soa* b, int device, rt_s
   std::vector<double> tu(s->tex_u, s->tex_u + s->n_tex_coords), tv(s->tex_v, s->tex_v + s->n_tex_coords);
   std::vector<unsigned char> texels(s->texels, s->texels + 3 * s->n_texels);
 
+  tick("misc");
   HIP_TRY(hipSetDevice(device));
   auto* sc = new rt_scene();
   sc->device = device;

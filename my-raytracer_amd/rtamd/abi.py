@@ -112,9 +112,17 @@ class GenParams(C.Structure):
                 ("seed", C.c_ulonglong), ("max_depth", C.c_int), ("detail", C.c_int)]
 
 
+class UploadOptions(C.Structure):
+    _fields_ = [("device_tree", C.c_int), ("reserved_", C.c_int * 7)]
+
+
+RT_TREE_SAH, RT_TREE_REFERENCE = 0, 1
+
 # Symbols each library must export (declared in include/*.h).
 HIP_SYMBOLS = {
     "rt_scene_upload": (C.c_int, [C.POINTER(SceneSoA), C.POINTER(BvhSoA), C.c_int, C.POINTER(C.c_void_p)]),
+    "rt_scene_upload_ex": (C.c_int, [C.POINTER(SceneSoA), C.POINTER(BvhSoA), C.c_int, C.POINTER(UploadOptions),
+                                     C.POINTER(C.c_void_p)]),
     "rt_scene_set_analytic": (C.c_int, [C.c_void_p, C.POINTER(Sphere), C.c_int, C.POINTER(Plane), C.c_int]),
     "rt_scene_device_bytes": (C.c_longlong, [C.c_void_p]),
     "rt_rows_in_shard": (C.c_int, [C.POINTER(RenderParams)]),

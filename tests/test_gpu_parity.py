@@ -36,12 +36,17 @@ class Case:
     cache = {}
 
     @classmethod
-    def get(cls, kind, **kw):
-        key = (kind, tuple(sorted(kw.items())))
+    def get(cls, kind, tree=None, **kw):
+        key = (kind, tree, tuple(sorted(kw.items())))
         if key not in cls.cache:
-            hs = rtamd.HostScene.generate(kind, **kw)
-            hs.prepare()
-            cls.cache[key] = (hs, rtamd.DeviceScene(hs, 0), pyoracle.Oracle(hs.raw, hs))
+            base = (kind, None, tuple(sorted(kw.items())))
+            if tree is not None and base in cls.cache:
+                hs, _, orc = cls.cache[base]
+            else:
+                hs = rtamd.HostScene.generate(kind, **kw)
+                hs.prepare()
+                orc = pyoracle.Oracle(hs.raw, hs)
+            cls.cache[key] = (hs, rtamd.DeviceScene(hs, 0, tree=tree), orc)
         return cls.cache[key]
 
 
@@ -87,8 +92,9 @@ def test_scene_goldens(fname, kind, kw, w, h, spp):
     ("office", {}, 64, 36, 3),
     ("random_tris", {"n_triangles": 20000}, 160, 90, 1),
 ])
-def test_parity_with_oracle(kind, kw, w, h, spp):
-    hs, dev, orc = Case.get(kind, **kw)
+@pytest.mark.parametrize("tree", [None, "reference"])
+def test_parity_with_oracle(kind, kw, w, h, spp, tree):
+    hs, dev, orc = Case.get(kind, tree=tree, **kw)
     p = hs.render_params(w, h, spp)
     ref, cnt = orc.render(p, pyoracle.MODE_REFERENCE)
     p.out_format = rtamd.RT_OUT_RGB_F64
@@ -103,8 +109,9 @@ def test_parity_with_oracle(kind, kw, w, h, spp):
 
 @pytest.mark.parametrize("kind,kw,w,h", [("cornell", {}, 160, 120), ("office", {}, 192, 108),
                                          ("random_tris", {"n_triangles": 20000}, 160, 90)])
-def test_traversal_counters_match_oracle_replica(kind, kw, w, h):
-    hs, dev, orc = Case.get(kind, **kw)
+@pytest.mark.parametrize("tree", [None, "reference"])
+def test_traversal_counters_match_oracle_replica(kind, kw, w, h, tree):
+    hs, dev, orc = Case.get(kind, tree=tree, **kw)
     p = hs.render_params(w, h, 1)
     p.flags = rtamd.RT_FLAG_TRAVERSAL_STATS
     _, st = dev.render(p)
@@ -446,3 +453,43 @@ def test_analytic_bad_arguments_fail_loudly():
         dev.set_analytic(None, 1, None, 0)
     with pytest.raises(rtamd.RtError):
         dev.set_analytic(None, 0, None, -1)
+
+
+# ---- device traversal hierarchy (rt_upload_options.device_tree) ----
+@pytest.mark.parametrize("kind,kw,w,h,spp", [("office", {}, 320, 180, 1), ("cornell", {"detail": 3}, 97, 61, 2),
+                                             ("random_tris", {"n_triangles": 20000}, 160, 90, 1)])
+def test_device_tree_changes_no_pixel(kind, kw, w, h, spp):
+    # The closest hit is the smallest (t, reference slot) over a conservative superset of
+    # candidates, so the SAH hierarchy and the refined reference tree give identical bits.
+    hs, sah, _ = Case.get(kind, **kw)
+    _, ref, _ = Case.get(kind, tree="reference", **kw)
+    p = hs.render_params(w, h, spp)
+    p.out_format = rtamd.RT_OUT_RGB_F64
+    a, sa = sah.render(p)
+    b, sb = ref.render(p)
+    assert np.array_equal(a, b) and counts(sa) == counts(sb)
+    p.flags = rtamd.RT_FLAG_WIDE_STATS
+    _, wa = sah.render(p)
+    _, wb = ref.render(p)
+    assert wa.node_visits < wb.node_visits   # the point of the option
+
+
+def test_sah_tree_independent_of_build_threads(monkeypatch):
+    hs = rtamd.HostScene.generate("random_tris", n_triangles=300000, seed=5)
+    hs.prepare()
+    p = hs.render_params(192, 108, 1)
+    p.flags = rtamd.RT_FLAG_WIDE_STATS
+    out = []
+    for t in ("1", "7"):
+        monkeypatch.setenv("RT_BUILD_THREADS", t)
+        dev = rtamd.DeviceScene(hs, 0, tree="sah")
+        img, st = dev.render(p)
+        out.append((img, st.node_visits, st.tri_tests, dev.device_bytes))
+        dev.close()
+    assert np.array_equal(out[0][0], out[1][0]) and out[0][1:] == out[1][1:]
+
+
+def test_unknown_device_tree_fails_loudly():
+    hs, _, _ = Case.get("cornell")
+    with pytest.raises(ValueError):
+        rtamd.DeviceScene(hs, 0, tree="kd")
