@@ -8,10 +8,12 @@ One step = one full frame: every rank renders its interleaved 16-row stripes
 (stripe = rank mod N) with one launch of the flattened HIP kernel, then rank 0
 gathers the stripes over RCCL (torch.distributed "nccl") and re-interleaves
 them into the final image.  Total work per step is fixed => "strong" scaling.
-Consecutive frames are issued round-robin on --streams HIP streams (default 4,
-each with its own output buffer; the scene keeps one launch context per
-in-flight frame), so the drain at the end of one frame overlaps the next
-frame's work; every frame still traces all of its rays.
+Consecutive frames are rendered --frames at a time (default 8) by ONE launch
+of the persistent kernel (rt_launch_frames: the frames share one work queue,
+so the drain at the end of a launch is paid once per F frames); every frame
+still traces all of its rays.  --streams S > 1 additionally keeps S launches in
+flight on separate streams (default 1: launches serial, so the HIP-event launch
+duration is the kernel's own duration, as rocprofv3 reports it).
 
 Rays per frame are the canonical counts returned by the kernel's
 counters in an untimed launch.  Roofline: algorithmic bytes per launch =
@@ -53,8 +55,8 @@ STRIPE_H = 16
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=32)
+    ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--scene", default="office")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
@@ -64,7 +66,11 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="cpu_baseline: minimum timed CPU work")
     ap.add_argument("--save", default="", help="rank 0: save the gathered image (.npy)")
-    ap.add_argument("--streams", type=int, default=4, help="frames in flight (1 = strictly serial frames)")
+    ap.add_argument("--frames", type=int, default=8,
+                    help="frames per launch (rt_launch_frames, <= 8): one persistent-kernel launch renders F "
+                         "consecutive frames from one work queue, so the per-launch drain is paid once per F")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="launches in flight on separate streams (1 = launches strictly serial)")
     ap.add_argument("--tree", choices=["sah", "reference"], default="sah",
                     help="device traversal hierarchy (pixels identical either way; DESIGN.md §4)")
     ap.add_argument("--analytic", action="store_true",
@@ -102,15 +108,22 @@ def main():
     params.stripe_index = rank
     W = a.width
     S = max(1, min(a.streams, 8))   # librt_hip keeps 8 launch contexts per scene
+    F = 1 if a.adaptive else max(1, min(a.frames, rtamd.abi.RT_MAX_FRAMES))
     bufs = [torch.zeros((shard_max_rows(a.height, STRIPE_H, n), W, 3), dtype=torch.float32, device="cuda")
-            for _ in range(S)]
+            for _ in range(S * F)]
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(S - 1)]
     buf = bufs[0]
     stream = streams[0].cuda_stream
     prims = [torch.zeros((a.height, W, 3), dtype=torch.float64, device="cuda") for _ in range(S)] if a.adaptive else []
 
     # ---- counters: canonical rays + algorithmic bytes (untimed launches) ----
-    st = gpu.launch(params, buf.data_ptr(), stats=True, stream=stream)
+    if F > 1:   # same launch shape as the timed ones (identical frames: counts / F are exact)
+        st = gpu.launch_frames(params, [b.data_ptr() for b in bufs[:F]], stats=True, stream=stream)
+        for f in ("primary_rays", "shadow_rays", "reflection_rays", "node_visits", "tri_tests", "closest_hits",
+                  "pixels"):
+            setattr(st, f, getattr(st, f) // F)
+    else:
+        st = gpu.launch(params, buf.data_ptr(), stats=True, stream=stream)
     params.flags = rtamd.RT_FLAG_TRAVERSAL_STATS
     tst = gpu.launch(params, buf.data_ptr(), stats=True, stream=stream)
     params.flags = rtamd.RT_FLAG_WIDE_STATS   # the production kernel's own node / triangle fetches
@@ -134,43 +147,55 @@ def main():
     gather = StripeGather(a.height, W, STRIPE_H, n, rank, device="cuda")
     image = None
 
-    starts, ends = [], []
+    starts, ends, launch_frames = [], [], []
 
-    def step(k, timed):
+    def launch(li, nf, timed):
+        """Launch li renders nf frames (steps); each frame is then gathered to rank 0."""
         nonlocal image
-        s = streams[k % S]
-        b = bufs[k % S]
+        s = streams[li % S]
+        bs = bufs[(li % S) * F:(li % S) * F + nf]
         with torch.cuda.stream(s):
             if timed:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(s)
             if a.adaptive:
-                gpu.launch(p64, prims[k % S].data_ptr(), stats=False, stream=s.cuda_stream)
-                gpu.launch_adaptive(params, prims[k % S].data_ptr(), b.data_ptr(), 4, 0.02, stats=False,
+                gpu.launch(p64, prims[li % S].data_ptr(), stats=False, stream=s.cuda_stream)
+                gpu.launch_adaptive(params, prims[li % S].data_ptr(), bs[0].data_ptr(), 4, 0.02, stats=False,
                                     stream=s.cuda_stream)
+            elif nf == 1:
+                gpu.launch(params, bs[0].data_ptr(), stats=False, stream=s.cuda_stream)
             else:
-                gpu.launch(params, b.data_ptr(), stats=False, stream=s.cuda_stream)
+                gpu.launch_frames(params, [b.data_ptr() for b in bs], stats=False, stream=s.cuda_stream)
             if timed:
                 e1.record(s)
                 starts.append(e0)
                 ends.append(e1)
-            image = gather(b)   # N>1: RCCL gather of the stripes to rank 0 + re-interleave
+                launch_frames.append(nf)
+            for b in bs:
+                image = gather(b)   # N>1: RCCL gather of the stripes to rank 0 + re-interleave
 
-    for k in range(a.warmup):
-        step(k, False)
+    def run(steps, timed):
+        li, done = 0, 0
+        while done < steps:
+            nf = min(F, steps - done)
+            launch(li, nf, timed)
+            li += 1
+            done += nf
+
+    run(a.warmup, False)
     torch.cuda.synchronize()
     if n > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(a.steps):
-        step(k, True)
+    run(a.steps, True)
     if n > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     kernel_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
     kernel_ms_avg = float(np.mean(kernel_ms))
+    frames_per_launch = float(np.mean(launch_frames))
 
     tot = torch.tensor([rays_local, alg_bytes_local], dtype=torch.float64, device="cuda")
     tmax = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -185,7 +210,7 @@ def main():
             np.save(a.save, image.float().cpu().numpy())
         ms_per_step = elapsed / a.steps * 1e3
         mrays = rays_total * a.steps / elapsed / 1e6
-        achieved = alg_bytes_local / (kernel_ms_avg * 1e-3) / 1e9
+        achieved = alg_bytes_local * frames_per_launch / (kernel_ms_avg * 1e-3) / 1e9
         achieved_interval = alg_bytes_local / (elapsed / a.steps) / 1e9
         out = {
             "metric": "Mrays/sec (primary+shadow+reflect), Office 1920x1080 1spp",
@@ -211,7 +236,8 @@ def main():
                 "rays_breakdown_rank0": {"primary": st.primary_rays, "shadow": st.shadow_rays,
                                          "reflection": st.reflection_rays},
                 "parallelism": f"row-stripes x{n} (16-row interleave) + RCCL gather" if n > 1 else "single GPU",
-                "frames_in_flight": S,
+                "frames_per_launch": F,
+                "launches_in_flight": S,
                 "adaptive_pass": adaptive_info,
                 "analytic_prims": bool(gpu.analytic),
                 "host_bvh_build_s": round(build_s, 4),
@@ -226,18 +252,22 @@ def main():
                 "traffic": None,
                 "kernel_ms_avg": round(kernel_ms_avg, 4),
                 "achieved_per_frame_interval": round(achieved_interval, 1),
-                "note": "achieved = alg bytes / mean launch duration (launches of consecutive frames overlap); "
-                        "achieved_per_frame_interval = alg bytes / (elapsed / steps)",
-                "alg_bytes_per_launch": int(alg_bytes_local),
-                "alg_bytes_def": "64*node_visits + 48*tri_tests + 64*closest_hits (rank-0 launch)",
+                "note": "achieved = alg bytes per launch (frames_per_launch frames) / mean launch duration "
+                        "(HIP events on the launch stream); achieved_per_frame_interval = alg bytes per frame / "
+                        "(elapsed / steps)",
+                "alg_bytes_per_frame": int(alg_bytes_local),
+                "alg_bytes_per_launch": int(alg_bytes_local * frames_per_launch),
+                "alg_bytes_def": "64*node_visits + 48*tri_tests + 64*closest_hits (rank-0 frame, canonical 2-wide "
+                                 "traversal of the reference tree)",
                 # The scene (nodes + triangles, a few MB) stays cache-resident: the canonical
                 # stream is served by L1 (98 % hits) and L2, so frac vs HBM exceeds 1 (SURVEY §8d
                 # caveat).  The binding roof is the CU's L1 data path; it is priced with the
                 # bytes the production kernel actually fetches.
                 "l1_roof": {"peak": round(L1_PEAK_GBPS, 1), "unit": "GB/s",
-                            "fetch_bytes_per_launch": int(fetch_bytes_local),
-                            "achieved": round(fetch_bytes_local / (kernel_ms_avg * 1e-3) / 1e9, 1),
-                            "frac": round(fetch_bytes_local / (kernel_ms_avg * 1e-3) / 1e9 / L1_PEAK_GBPS, 4),
+                            "fetch_bytes_per_launch": int(fetch_bytes_local * frames_per_launch),
+                            "achieved": round(fetch_bytes_local * frames_per_launch / (kernel_ms_avg * 1e-3) / 1e9, 1),
+                            "frac": round(fetch_bytes_local * frames_per_launch / (kernel_ms_avg * 1e-3) / 1e9
+                                          / L1_PEAK_GBPS, 4),
                             "achieved_per_frame_interval": round(fetch_bytes_local / (elapsed / a.steps) / 1e9, 1),
                             "frac_per_frame_interval": round(fetch_bytes_local / (elapsed / a.steps) / 1e9
                                                              / L1_PEAK_GBPS, 4),

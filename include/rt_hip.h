@@ -186,6 +186,16 @@ int rt_rows_in_shard(const rt_render_params* p);
 int rt_launch_compute_image(rt_scene* scene, const rt_render_params* p, void* d_out,
                             rt_stats* stats, void* stream);
 
+/* Up to RT_MAX_FRAMES frames in ONE launch of the persistent kernel: frame f renders
+ * p[f] into d_outs[f].  The frames share one work queue, so the tail of one frame is
+ * filled with the next frame's pixels instead of idling (the per-launch drain is paid
+ * once per batch).  p[f] may differ from p[0] only in camera.eye / lower_left / x_dir /
+ * y_dir (an animation path); everything else must be identical.  stats (optional,
+ * synchronising) sums the frames.  Results equal n_frames rt_launch_compute_image calls. */
+#define RT_MAX_FRAMES 8
+int rt_launch_frames(rt_scene* scene, const rt_render_params* p, int n_frames, void* const* d_outs,
+                     rt_stats* stats, void* stream);
+
 /* Adaptive supersampling pass: replaces adaptive_supersampling_device
  * (mytracer_gpu.cu:162-229, launched at :83-109 with subp = 4, threshold = 0.02).
  * d_primary: the primary pass of the SAME params rendered with

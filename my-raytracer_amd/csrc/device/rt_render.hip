@@ -120,6 +120,10 @@ enum : int {
 };
 constexpr unsigned kGuardIters = 1u << 24;   // persistent-loop watchdog (never reached by a correct kernel)
 
+constexpr int kMaxFrames = RT_MAX_FRAMES;   // frames per launch (kernel-argument tables)
+struct FrameCam {
+  double eye[3], ll[3], xd[3], yd[3];
+};
 struct KParams {
   const GNode* nodes;
   const GNode4* nodes4;
@@ -137,13 +141,11 @@ struct KParams {
   uint32_t* spill;      // [stack_words][nslots] traversal-stack entries below the LDS ring
   unsigned long long* wavelog;  // STATS: per wave {start, last refill, end, pixels} (s_memrealtime)
   const double* lights; // [n_lights][6] position xyz, colour rgb
-  void* out;
   size_t nslots;
   int n_gnodes;
   int out_fmt;
   int pad0[2];
   double root_lo[3], root_hi[3];
-  double eye[3], ll[3], xd[3], yd[3];
   int W, H;
   int n_lights, max_depth;
   double bg[3], amb[3];
@@ -161,6 +163,12 @@ struct KParams {
   int nsamp;
   int n_prims;              // analytic primitives (0 unless rt_scene_set_analytic)
   const GPrim* prims;
+  // frames of this launch (rt_launch_frames): work item w belongs to frame w / (64 * frame_tiles)
+  int n_frames;
+  int pad3;
+  long long frame_tiles;
+  FrameCam cam[kMaxFrames];
+  void* out[kMaxFrames];
 };
 
 // ---- fp64 vector ops (course vec4 semantics on xyz) ----
@@ -356,7 +364,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
 
   // ---- per-lane state live across phases ----
   int state = ST_FETCH;
-  int px = 0, lrow = 0, py = 0, sample = 0, depth = 0, light = 0, mesh = 0, item = 0;
+  int px = 0, lrow = 0, py = 0, sample = 0, depth = 0, light = 0, mesh = 0, item = 0, frame = 0;
   int best = kNoHit;        // device record of the closest hit
   int best_slot = kNoHit;   // its reference slot (tie-break key)
   double thit = DBL_MAX;
@@ -389,14 +397,15 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
     const double xo = (si) / (double)n - 0.5 + 1.0 / (2.0 * n);
     const double yo = (sj) / (double)n - 0.5 + 1.0 / (2.0 * n);
     const double X = (double)px + xo, Y = (double)py + yo;
-    const D3 dir = d3(P.ll[0] + X * P.xd[0] + Y * P.yd[0] - P.eye[0],
-                      P.ll[1] + X * P.xd[1] + Y * P.yd[1] - P.eye[1],
-                      P.ll[2] + X * P.xd[2] + Y * P.yd[2] - P.eye[2]);
+    const FrameCam& K = P.cam[frame];
+    const D3 dir = d3(K.ll[0] + X * K.xd[0] + Y * K.yd[0] - K.eye[0],
+                      K.ll[1] + X * K.xd[1] + Y * K.yd[1] - K.eye[1],
+                      K.ll[2] + X * K.xd[2] + Y * K.yd[2] - K.eye[2]);
     ST3(F_SCOL, d3(0, 0, 0));
     ST(F_W, 1.0);
     depth = 0;
     c_primary++;
-    emit_ray(d3(P.eye[0], P.eye[1], P.eye[2]), dir, DBL_MAX);
+    emit_ray(d3(K.eye[0], K.eye[1], K.eye[2]), dir, DBL_MAX);
     state = ST_CLOSEST;
   };
 
@@ -434,8 +443,10 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
             lrow = id != 0xffffffffu ? (int)(id / (uint32_t)P.W) : P.rows;
             item = (int)wk;
           } else {
-            const long long tile = wk >> 6;
+            long long tile = wk >> 6;
             const int j = (int)(wk & 63);
+            frame = P.n_frames > 1 ? (int)(tile / P.frame_tiles) : 0;
+            tile -= (long long)frame * P.frame_tiles;
             const long long ty = tile / P.tiles_x;
             const int tx = (int)(tile - ty * P.tiles_x);
             px = tx * 8 + (j & 7);
@@ -931,10 +942,10 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
           const double r = stdmin(pcol.x / nn, 1.0), g = stdmin(pcol.y / nn, 1.0), b = stdmin(pcol.z / nn, 1.0);
           const size_t o = 3 * ((size_t)lrow * P.W + px);
           if (P.out_fmt == RT_OUT_RGB_F64) {
-            double* out = reinterpret_cast<double*>(P.out) + o;
+            double* out = reinterpret_cast<double*>(P.out[frame]) + o;
             out[0] = r; out[1] = g; out[2] = b;
           } else {
-            float* out = reinterpret_cast<float*>(P.out) + o;
+            float* out = reinterpret_cast<float*>(P.out[frame]) + o;
             out[0] = (float)r; out[1] = (float)g; out[2] = (float)b;
           }
           state = heads_left > 0 ? ST_FETCH : ST_DONE;
@@ -1990,10 +2001,24 @@ int rt_rows_in_shard(const rt_render_params* p) {
 namespace {
 // One render launch; list != nullptr: adaptive pass over the pixel ids list[0 .. *count)
 // (at most list_cap of them) of the full frame.
-int launch_render(rt_scene* sc, const rt_render_params* p, void* d_out, rt_stats* stats, void* stream,
-                  const uint32_t* list, const unsigned long long* count, long long list_cap,
+// n_frames > 1 (rt_launch_frames): params p[0..n_frames) differ only in their camera vectors,
+// frame f is written to outs[f].
+int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* const* outs, rt_stats* stats,
+                  void* stream, const uint32_t* list, const unsigned long long* count, long long list_cap,
                   double* sample_out = nullptr) {
-  if (!sc || !p || !d_out) return fail(RT_ERR_INVALID, "rt_launch_compute_image: null argument");
+  if (!sc || !p || !outs) return fail(RT_ERR_INVALID, "rt_launch_compute_image: null argument");
+  if (n_frames < 1 || n_frames > kMaxFrames) return fail(RT_ERR_INVALID, "rt_launch_frames: n_frames out of range");
+  for (int f = 0; f < n_frames; ++f) {
+    if (!outs[f]) return fail(RT_ERR_INVALID, "rt_launch_compute_image: null output buffer");
+    if (f == 0) continue;
+    rt_render_params q = p[f];   // everything but the camera vectors must match frame 0
+    for (int k = 0; k < 3; ++k) {
+      q.camera.eye[k] = p[0].camera.eye[k]; q.camera.lower_left[k] = p[0].camera.lower_left[k];
+      q.camera.x_dir[k] = p[0].camera.x_dir[k]; q.camera.y_dir[k] = p[0].camera.y_dir[k];
+    }
+    if (std::memcmp(&q, &p[0], sizeof q) != 0)
+      return fail(RT_ERR_INVALID, "rt_launch_frames: frames may differ only in camera position and direction");
+  }
   if (p->camera.width <= 0 || p->camera.height <= 0) return fail(RT_ERR_INVALID, "bad image size");
   if (p->n_lights < 0 || p->n_lights > RT_MAX_LIGHTS) return fail(RT_ERR_INVALID, "n_lights out of range");
   if (p->spp_n < 1 || p->spp_n > 64) return fail(RT_ERR_INVALID, "spp_n must be in [1, 64]");
@@ -2015,13 +2040,18 @@ int launch_render(rt_scene* sc, const rt_render_params* p, void* d_out, rt_stats
   LaunchCtx& C = sc->ctx[sc->next_ctx];
   const int ci = sc->next_ctx;
   P.ctr = C.d_ctr;
-  P.out = d_out;
+  P.n_frames = n_frames;
+  for (int f = 0; f < n_frames; ++f) {
+    P.out[f] = outs[f];
+    for (int k = 0; k < 3; ++k) {
+      P.cam[f].eye[k] = p[f].camera.eye[k]; P.cam[f].ll[k] = p[f].camera.lower_left[k];
+      P.cam[f].xd[k] = p[f].camera.x_dir[k]; P.cam[f].yd[k] = p[f].camera.y_dir[k];
+    }
+  }
   P.n_gnodes = sc->n_gnodes;
   P.out_fmt = p->out_format;
   for (int k = 0; k < 3; ++k) {
     P.root_lo[k] = sc->root_lo[k]; P.root_hi[k] = sc->root_hi[k];
-    P.eye[k] = p->camera.eye[k]; P.ll[k] = p->camera.lower_left[k];
-    P.xd[k] = p->camera.x_dir[k]; P.yd[k] = p->camera.y_dir[k];
     P.bg[k] = p->background[k]; P.amb[k] = p->ambience[k];
   }
   P.W = p->camera.width;
@@ -2052,7 +2082,8 @@ int launch_render(rt_scene* sc, const rt_render_params* p, void* d_out, rt_stats
   P.rows = rows;
   P.tiles_x = (P.W + 7) / 8;
   P.nsamp = p->spp_n * p->spp_n;
-  P.n_tiles = list ? (list_cap * P.nsamp + 63) / 64 : (long long)P.tiles_x * ((rows + 7) / 8);
+  P.frame_tiles = list ? (list_cap * P.nsamp + 63) / 64 : (long long)P.tiles_x * ((rows + 7) / 8);
+  P.n_tiles = P.frame_tiles * n_frames;
   P.list = list;
   P.list_count = count;
   P.sample_out = sample_out;
@@ -2098,7 +2129,12 @@ int launch_render(rt_scene* sc, const rt_render_params* p, void* d_out, rt_stats
 extern "C" {
 
 int rt_launch_compute_image(rt_scene* sc, const rt_render_params* p, void* d_out, rt_stats* stats, void* stream) {
-  return launch_render(sc, p, d_out, stats, stream, nullptr, nullptr, 0);
+  return launch_render(sc, p, 1, &d_out, stats, stream, nullptr, nullptr, 0);
+}
+
+int rt_launch_frames(rt_scene* sc, const rt_render_params* p, int n_frames, void* const* d_outs, rt_stats* stats,
+                     void* stream) {
+  return launch_render(sc, p, n_frames, d_outs, stats, stream, nullptr, nullptr, 0);
 }
 
 int rt_launch_adaptive(rt_scene* sc, const rt_render_params* p, const double* d_primary, void* d_out, int subp,
@@ -2134,7 +2170,7 @@ int rt_launch_adaptive(rt_scene* sc, const rt_render_params* p, const double* d_
   q.stripe_index = 0;
   q.row_begin = 0;
   q.row_end = H;
-  int rc = launch_render(sc, &q, d_out, stats, stream, list, cnt, cap, samples);
+  int rc = launch_render(sc, &q, 1, &d_out, stats, stream, list, cnt, cap, samples);
   if (rc == RT_OK && cap > 0) {
     hipLaunchKernelGGL(adaptive_reduce_kernel, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, st, list, cnt,
                        samples, nsamp, d_out, p->out_format);

@@ -227,6 +227,21 @@ class DeviceScene:
                    "rt_launch_compute_image")
         return st
 
+    def launch_frames(self, params, d_outs, stats=False, stream=None):
+        """Asynchronous render of len(d_outs) frames in ONE launch (rt_launch_frames); params is
+        one RenderParams (every frame the same) or a list of them differing only in their camera
+        vectors.  Returns Stats summed over the frames if stats=True."""
+        n = len(d_outs)
+        plist = params if isinstance(params, (list, tuple)) else [params] * n
+        if len(plist) != n:
+            raise ValueError("one params per output buffer")
+        parr = (abi.RenderParams * n)(*plist)
+        oarr = (C.c_void_p * n)(*[C.c_void_p(d) for d in d_outs])
+        st = abi.Stats() if stats else None
+        _check_hip(hip_lib().rt_launch_frames(self._h, parr, n, oarr, C.byref(st) if st is not None else None,
+                                              C.c_void_p(stream) if stream else None), "rt_launch_frames")
+        return st
+
     def launch_adaptive(self, params, d_primary, d_out, subp=4, threshold=0.02, stats=False, stream=None):
         """Adaptive supersampling pass (rt_launch_adaptive) over device buffers (int pointers);
         returns (Stats or None, number of re-rendered pixels)."""

@@ -12,6 +12,7 @@ RT_ERR_INVALID = -1
 RT_ERR_HIP = -2
 RT_ERR_UNSUPPORTED = -3
 RT_MAX_LIGHTS = 16
+RT_MAX_FRAMES = 8
 RT_DRAW_FLAT = 0
 RT_DRAW_PHONG = 1
 RT_OUT_RGB_F32 = 0
@@ -128,6 +129,8 @@ HIP_SYMBOLS = {
     "rt_rows_in_shard": (C.c_int, [C.POINTER(RenderParams)]),
     "rt_launch_compute_image": (C.c_int, [C.c_void_p, C.POINTER(RenderParams), C.c_void_p,
                                           C.POINTER(Stats), C.c_void_p]),
+    "rt_launch_frames": (C.c_int, [C.c_void_p, C.POINTER(RenderParams), C.c_int, C.POINTER(C.c_void_p),
+                                   C.POINTER(Stats), C.c_void_p]),
     "rt_launch_adaptive": (C.c_int, [C.c_void_p, C.POINTER(RenderParams), C.c_void_p, C.c_void_p, C.c_int,
                                      C.c_double, C.POINTER(Stats), C.POINTER(C.c_longlong), C.c_void_p]),
     "rt_render_to_host": (C.c_int, [C.c_void_p, C.POINTER(RenderParams), C.c_void_p, C.POINTER(Stats)]),

@@ -493,3 +493,52 @@ def test_unknown_device_tree_fails_loudly():
     hs, _, _ = Case.get("cornell")
     with pytest.raises(ValueError):
         rtamd.DeviceScene(hs, 0, tree="kd")
+
+
+# ---- several frames in one launch (rt_launch_frames) ----
+def _moved(p, dx):
+    q = rtamd.abi.RenderParams.from_buffer_copy(p)
+    for k, v in enumerate((dx, 0.5 * dx, -dx)):
+        q.camera.eye[k] += v
+        q.camera.lower_left[k] += v
+    return q
+
+
+@pytest.mark.parametrize("stripes", [1, 3])
+def test_frames_in_one_launch_equal_single_launches(stripes):
+    import torch
+
+    hs, dev, _ = Case.get("office")
+    p = hs.render_params(200, 113, 1)
+    p.out_format = rtamd.RT_OUT_RGB_F64
+    if stripes > 1:
+        p.stripe_height, p.stripe_count, p.stripe_index = 16, stripes, 1
+    frames = [_moved(p, 0.07 * f) for f in range(5)]
+    rows = rtamd.rows_in_shard(p)
+    singles, tot = [], [0, 0, 0]
+    for q in frames:
+        img, st = dev.render(q)
+        singles.append(img)
+        tot = [a + b for a, b in zip(tot, counts(st))]
+    outs = [torch.zeros((rows, 200, 3), dtype=torch.float64, device="cuda") for _ in frames]
+    st = dev.launch_frames(frames, [o.data_ptr() for o in outs], stats=True)
+    for o, ref in zip(outs, singles):
+        assert np.array_equal(o.cpu().numpy(), ref)
+    assert counts(st) == tot
+    assert not np.array_equal(singles[0], singles[4])   # the cameras really differ
+
+
+def test_frames_launch_rejects_mismatched_frames():
+    import torch
+
+    hs, dev, _ = Case.get("cornell")
+    p = hs.render_params(32, 24, 1)
+    o = [torch.zeros((24, 32, 3), device="cuda") for _ in range(9)]
+    q = rtamd.abi.RenderParams.from_buffer_copy(p)
+    q.max_depth = p.max_depth + 1
+    with pytest.raises(rtamd.RtError):
+        dev.launch_frames([p, q], [o[0].data_ptr(), o[1].data_ptr()])
+    with pytest.raises(rtamd.RtError):
+        dev.launch_frames(p, [x.data_ptr() for x in o])          # more than RT_MAX_FRAMES
+    with pytest.raises(rtamd.RtError):
+        dev.launch_frames(p, [o[0].data_ptr(), 0])              # null output

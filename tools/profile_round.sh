@@ -6,11 +6,11 @@ set -e -o pipefail
 TAG=${1:?tag}
 O=gpurun_out
 export TMPDIR=/tmp
-B="python bench.py --steps 5 --warmup 1 --no-cpu-baseline --streams 1"
-timeout -k 10 300 python bench.py --steps 20 --warmup 3 > $O/bench_$TAG.json 2> $O/bench_$TAG.err
-timeout -k 10 300 python bench.py --steps 20 --warmup 3 --streams 1 --no-cpu-baseline > $O/bench_${TAG}_serial.json 2>> $O/bench_$TAG.err
+B="python bench.py --steps 5 --warmup 1 --no-cpu-baseline --frames 1"
+timeout -k 10 300 python bench.py --steps 32 --warmup 8 > $O/bench_$TAG.json 2> $O/bench_$TAG.err
+timeout -k 10 300 python bench.py --steps 32 --warmup 8 --frames 1 --no-cpu-baseline > $O/bench_${TAG}_serial.json 2>> $O/bench_$TAG.err
 # kernel trace of the bench's own default command (frames in flight) and of serial frames
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$TAG -o run -- python bench.py --steps 20 --warmup 3 --no-cpu-baseline > $O/prof_$TAG.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$TAG -o run -- python bench.py --steps 32 --warmup 8 --no-cpu-baseline > $O/prof_$TAG.log 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_${TAG}_serial -o run -- $B > $O/prof_${TAG}_serial.log 2>&1
 pass() {
   local name=$1; shift
