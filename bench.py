@@ -206,6 +206,7 @@ def main():
     elapsed = float(tmax[0])
 
     if rank == 0:
+        traffic = pmc_traffic(a, n, F)
         if a.save:
             np.save(a.save, image.float().cpu().numpy())
         ms_per_step = elapsed / a.steps * 1e3
@@ -249,7 +250,8 @@ def main():
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                "traffic": None,
+                "traffic": traffic["bytes_per_launch"] if traffic else None,
+                "traffic_detail": traffic,
                 "kernel_ms_avg": round(kernel_ms_avg, 4),
                 "achieved_per_frame_interval": round(achieved_interval, 1),
                 "note": "achieved = alg bytes per launch (frames_per_launch frames) / mean launch duration "
@@ -281,6 +283,28 @@ def main():
     if n > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def pmc_traffic(a, n, F):
+    """HBM bytes per launch from the committed rocprofv3 --pmc summary of this exact launch
+    shape (profiles/r*/pmc_office1080.json: FETCH_SIZE x 2 (gfx950) + WRITE_SIZE, in bytes,
+    production kernel dispatches), or None when this run's shape was not profiled."""
+    default = (a.scene == "office" and a.width == 1920 and a.height == 1080 and a.spp == 1 and n == 1
+               and not a.adaptive and a.tree == "sah")
+    if not default:
+        return None
+    found = sorted(ROOT.glob("profiles/r*/pmc_office1080.json"))
+    if not found:
+        return None
+    d = json.loads(found[-1].read_text())
+    if d.get("_frames_per_launch") != F:
+        return None
+    der = d.get("_derived", {})
+    if "hbm_read_bytes_corrected" not in der or "hbm_write_bytes" not in der:
+        return None
+    return {"bytes_per_launch": int(der["hbm_read_bytes_corrected"] + der["hbm_write_bytes"]),
+            "read": int(der["hbm_read_bytes_corrected"]), "write": int(der["hbm_write_bytes"]),
+            "source": str(found[-1].relative_to(ROOT))}
 
 
 def cpu_baseline(host, params, a):

@@ -1,6 +1,7 @@
 """Summarise rocprofv3 --pmc passes of bench.py into one JSON (dev tool).
 
-usage: python tools/pmc_summary.py OUT.json DIR [DIR ...]
+usage: PMC_CMD="<profiled command>" PMC_FRAMES=<frames per launch> \
+       python tools/pmc_summary.py OUT.json DIR [DIR ...]
 Each DIR holds one pass's pmc_counter_collection.csv.  Only the production
 render kernel (render_kernel<4, false>) dispatches are averaged.  Derived
 figures follow MI355X_MICROARCH.md's HBM section: FETCH_SIZE / WRITE_SIZE are
@@ -57,8 +58,12 @@ def main():
     out, dirs = sys.argv[1], sys.argv[2:]
     c = collect(dirs)
     c["_derived"] = derive(c)
-    c["_note"] = ("rocprofv3 --pmc, one pass per directory (" + ", ".join(os.path.basename(d) for d in dirs)
-                  + ") of `python bench.py --steps 5 --warmup 1 --no-cpu-baseline`; production kernel only. "
+    cmd = os.environ.get("PMC_CMD", "python bench.py")
+    c["_command"] = cmd
+    c["_frames_per_launch"] = int(os.environ.get("PMC_FRAMES", "1"))
+    c["_note"] = ("rocprofv3 --pmc, one pass per directory ("
+                  + ", ".join(os.path.basename(os.path.normpath(d)) for d in dirs)
+                  + f") of `{cmd}`; production kernel dispatches only, per dispatch (= per launch). "
                   "FETCH_SIZE/WRITE_SIZE in KB; HBM read bytes = 2*FETCH_SIZE*1024 on gfx950.")
     with open(out, "w") as f:
         json.dump(c, f, indent=1)
