@@ -8,7 +8,7 @@ One step = one full frame: every rank renders its interleaved 16-row stripes
 (stripe = rank mod N) with one launch of the flattened HIP kernel, then rank 0
 gathers the stripes over RCCL (torch.distributed "nccl") and re-interleaves
 them into the final image.  Total work per step is fixed => "strong" scaling.
-Consecutive frames are rendered --frames at a time (default 8) by ONE launch
+Consecutive frames are rendered --frames at a time (default 8 per GPU) by ONE launch
 of the persistent kernel (rt_launch_frames: the frames share one work queue,
 so the drain at the end of a launch is paid once per F frames); every frame
 still traces all of its rays.  --streams S > 1 additionally keeps S launches in
@@ -66,9 +66,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="cpu_baseline: minimum timed CPU work")
     ap.add_argument("--save", default="", help="rank 0: save the gathered image (.npy)")
-    ap.add_argument("--frames", type=int, default=8,
-                    help="frames per launch (rt_launch_frames, <= 8): one persistent-kernel launch renders F "
-                         "consecutive frames from one work queue, so the per-launch drain is paid once per F")
+    ap.add_argument("--frames", type=int, default=0,
+                    help="frames per launch (rt_launch_frames, <= 64; default 8 x GPUs): one persistent-kernel "
+                         "launch renders F consecutive frames from one work queue, so the per-launch drain is "
+                         "paid once per F")
     ap.add_argument("--streams", type=int, default=1,
                     help="launches in flight on separate streams (1 = launches strictly serial)")
     ap.add_argument("--tree", choices=["sah", "reference"], default="sah",
@@ -108,9 +109,11 @@ def main():
     params.stripe_index = rank
     W = a.width
     S = max(1, min(a.streams, 8))   # librt_hip keeps 8 launch contexts per scene
-    F = 1 if a.adaptive else max(1, min(a.frames, rtamd.abi.RT_MAX_FRAMES))
-    bufs = [torch.zeros((shard_max_rows(a.height, STRIPE_H, n), W, 3), dtype=torch.float32, device="cuda")
-            for _ in range(S * F)]
+    F = 1 if a.adaptive else max(1, min(a.frames or 8 * n, rtamd.abi.RT_MAX_FRAMES))
+    # per stream: the F frames of one launch, contiguous, so one collective gathers them
+    fbufs = [torch.zeros((F, shard_max_rows(a.height, STRIPE_H, n), W, 3), dtype=torch.float32, device="cuda")
+             for _ in range(S)]
+    bufs = [fb[f] for fb in fbufs for f in range(F)]
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(S - 1)]
     buf = bufs[0]
     stream = streams[0].cuda_stream
@@ -144,7 +147,7 @@ def main():
     # bytes the production kernel requests from L1: 128-B GNode4, 80-B GTri, 32-B TriShade per hit
     fetch_bytes_local = 128 * wst.node_visits + 80 * wst.tri_tests + 32 * wst.closest_hits
 
-    gather = StripeGather(a.height, W, STRIPE_H, n, rank, device="cuda")
+    gather = StripeGather(a.height, W, STRIPE_H, n, rank, device="cuda", frames=F)
     image = None
 
     starts, ends, launch_frames = [], [], []
@@ -171,8 +174,7 @@ def main():
                 starts.append(e0)
                 ends.append(e1)
                 launch_frames.append(nf)
-            for b in bs:
-                image = gather(b)   # N>1: RCCL gather of the stripes to rank 0 + re-interleave
+            image = gather(fbufs[li % S])   # N>1: ONE RCCL gather of the F frames' stripes + re-interleave
 
     def run(steps, timed):
         li, done = 0, 0
@@ -208,7 +210,7 @@ def main():
     if rank == 0:
         traffic = pmc_traffic(a, n, F)
         if a.save:
-            np.save(a.save, image.float().cpu().numpy())
+            np.save(a.save, (image[0] if image.dim() == 4 else image).float().cpu().numpy())
         ms_per_step = elapsed / a.steps * 1e3
         mrays = rays_total * a.steps / elapsed / 1e6
         achieved = alg_bytes_local * frames_per_launch / (kernel_ms_avg * 1e-3) / 1e9

@@ -120,13 +120,20 @@ enum : int {
 };
 constexpr unsigned kGuardIters = 1u << 24;   // persistent-loop watchdog (never reached by a correct kernel)
 
-constexpr int kMaxFrames = RT_MAX_FRAMES;   // frames per launch (kernel-argument tables)
-struct FrameCam {
+constexpr int kMaxFrames = RT_MAX_FRAMES;   // frames per launch
+// per-frame camera and output buffer; a launch's table follows its counters in device memory
+struct FrameDesc {
   double eye[3], ll[3], xd[3], yd[3];
+  void* out;
+  long long pad;
 };
+static_assert(sizeof(FrameDesc) == 112, "FrameDesc must be 112 bytes");
+constexpr size_t kCtrBytes = kCtrWords * sizeof(unsigned long long);
+constexpr size_t kCtlBytes = kCtrBytes + kMaxFrames * sizeof(FrameDesc);
 struct KParams {
   const GNode* nodes;
   const GNode4* nodes4;
+  const GNode4Q* nodes4q;   // RT_QNODE builds only
   const GTri* tris;
   const uint32_t* slot2dev; // reference slot -> device record (2-wide canonical kernel)
   const TriShade* shade;
@@ -167,8 +174,7 @@ struct KParams {
   int n_frames;
   int pad3;
   long long frame_tiles;
-  FrameCam cam[kMaxFrames];
-  void* out[kMaxFrames];
+  const FrameDesc* frames;  // [n_frames]
 };
 
 // ---- fp64 vector ops (course vec4 semantics on xyz) ----
@@ -317,6 +323,10 @@ __device__ __forceinline__ uint32_t u4c(const uint4& v, int c) {
   return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
 }
 
+#ifndef RT_QNODE
+#define RT_QNODE 0   // 1: production traversal on quantised 64-B nodes (0: fp32 128-B nodes)
+#endif
+
 #ifndef RT_SPECULATIVE
 #define RT_SPECULATIVE 1   // 4-wide: postponed leaves + speculative node traversal
 #endif
@@ -397,7 +407,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
     const double xo = (si) / (double)n - 0.5 + 1.0 / (2.0 * n);
     const double yo = (sj) / (double)n - 0.5 + 1.0 / (2.0 * n);
     const double X = (double)px + xo, Y = (double)py + yo;
-    const FrameCam& K = P.cam[frame];
+    const FrameDesc& K = P.frames[frame];
     const D3 dir = d3(K.ll[0] + X * K.xd[0] + Y * K.yd[0] - K.eye[0],
                       K.ll[1] + X * K.xd[1] + Y * K.yd[1] - K.eye[1],
                       K.ll[2] + X * K.xd[2] + Y * K.yd[2] - K.eye[2]);
@@ -670,6 +680,29 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
           float k[4];
           uint32_t v[4];
           int cnt = 0;
+#if RT_QNODE
+          // quantised node: t = q * (scale * inv) + (origin * inv - o * inv); the scale is a
+          // power of two, so scale * inv is exact
+          const float4* nq = reinterpret_cast<const float4*>(P.nodes4q + cur);
+          const float4 a0 = nq[0], a1 = nq[1];
+          const uint4 qy = *reinterpret_cast<const uint4*>(nq + 2);
+          const uint4 rf = *reinterpret_cast<const uint4*>(nq + 3);
+          const float Ax = ivx * a0.w, Ay = ivy * a1.x, Az = ivz * a1.y;
+          const float Bx = __builtin_fmaf(a0.x, ivx, -oix), By = __builtin_fmaf(a0.y, ivy, -oiy),
+                      Bz = __builtin_fmaf(a0.z, ivz, -oiz);
+          const uint32_t qlx = __float_as_uint(a1.z), qhx = __float_as_uint(a1.w);
+          const uint32_t nqx = nxo ? qhx : qlx, fqx = nxo ? qlx : qhx;
+          const uint32_t nqy = nyo != 32u ? qy.y : qy.x, fqy = nyo != 32u ? qy.x : qy.y;
+          const uint32_t nqz = nzo != 64u ? qy.w : qy.z, fqz = nzo != 64u ? qy.z : qy.w;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const float tx0 = __builtin_fmaf((float)((nqx >> (8 * c)) & 255u), Ax, Bx);
+            const float tx1 = __builtin_fmaf((float)((fqx >> (8 * c)) & 255u), Ax, Bx);
+            const float ty0 = __builtin_fmaf((float)((nqy >> (8 * c)) & 255u), Ay, By);
+            const float ty1 = __builtin_fmaf((float)((fqy >> (8 * c)) & 255u), Ay, By);
+            const float tz0 = __builtin_fmaf((float)((nqz >> (8 * c)) & 255u), Az, Bz);
+            const float tz1 = __builtin_fmaf((float)((fqz >> (8 * c)) & 255u), Az, Bz);
+#else
           const char* nb = reinterpret_cast<const char*>(P.nodes4) + (size_t)cur * sizeof(GNode4);
           const float4 nx = *reinterpret_cast<const float4*>(nb + nxo);
           const float4 fx = *reinterpret_cast<const float4*>(nb + (nxo ^ 16u));
@@ -683,6 +716,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
             const float tx0 = __builtin_fmaf(f4c(nx, c), ivx, -oix), tx1 = __builtin_fmaf(f4c(fx, c), ivx, -oix);
             const float ty0 = __builtin_fmaf(f4c(ny, c), ivy, -oiy), ty1 = __builtin_fmaf(f4c(fy, c), ivy, -oiy);
             const float tz0 = __builtin_fmaf(f4c(nz, c), ivz, -oiz), tz1 = __builtin_fmaf(f4c(fz, c), ivz, -oiz);
+#endif
             const float tn = fmaxf(fmaxf(tx0, ty0), fmaxf(tz0, lo_c));
             const float tf = fminf(fminf(tx1, ty1), fminf(tz1, hi_c));
             const uint32_t r = u4c(rf, c);
@@ -942,10 +976,10 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
           const double r = stdmin(pcol.x / nn, 1.0), g = stdmin(pcol.y / nn, 1.0), b = stdmin(pcol.z / nn, 1.0);
           const size_t o = 3 * ((size_t)lrow * P.W + px);
           if (P.out_fmt == RT_OUT_RGB_F64) {
-            double* out = reinterpret_cast<double*>(P.out[frame]) + o;
+            double* out = reinterpret_cast<double*>(P.frames[frame].out) + o;
             out[0] = r; out[1] = g; out[2] = b;
           } else {
-            float* out = reinterpret_cast<float*>(P.out[frame]) + o;
+            float* out = reinterpret_cast<float*>(P.frames[frame].out) + o;
             out[0] = (float)r; out[1] = (float)g; out[2] = (float)b;
           }
           state = heads_left > 0 ? ST_FETCH : ST_DONE;
@@ -1203,7 +1237,9 @@ size_t lds_bytes(int stack_words) {
 // reused only after its previous launch completed (stream wait on `done`).
 constexpr int kContexts = 8;
 struct LaunchCtx {
-  unsigned long long* d_ctr = nullptr;       // [kCtrWords] work heads, stats, diagnostics
+  unsigned long long* d_ctr = nullptr;       // [kCtrWords] work heads, stats, diagnostics, then
+                                             // FrameDesc[kMaxFrames] (one H2D copy per launch)
+  unsigned char* h_ctl = nullptr;            // pinned staging of the same bytes
   double* d_pstate = nullptr;                // [nslots][kFields] path state
   uint32_t* d_spill = nullptr;               // [stack_words][nslots] (only when stack_words > kShortStack)
   unsigned long long* d_wavelog = nullptr;   // [nslots / 64][4]
@@ -1241,6 +1277,7 @@ struct rt_scene {
   int n_cu = 0;
   int blocks_per_cu[kNumVariants] = {0, 0, 0};
   GNode4* d_nodes4 = nullptr;
+  GNode4Q* d_nodes4q = nullptr;
   int n_gnodes4 = 0;
   std::vector<GMat> mesh_mats;  // host copy: the analytic materials are appended after these
   GPrim* d_prims = nullptr;     // analytic primitives (rt_scene_set_analytic), spheres then planes
@@ -1614,6 +1651,49 @@ void build_sah_tree(const rt_scene_soa* s, DevTree& E, std::vector<uint32_t>& de
   tick("merge");
 }
 
+// GNode4 -> GNode4Q: per axis, origin = union low corner (fp32), scale = the smallest power
+// of two with 255 * scale >= extent; child planes rounded outward onto the grid (exact in
+// double), so the decoded box contains the fp32 box.
+GNode4Q quantise_node(const GNode4& g) {
+  GNode4Q q;
+  std::memset(&q, 0, sizeof q);
+  const float* lo[3] = {g.lox, g.loy, g.loz};
+  const float* hi[3] = {g.hix, g.hiy, g.hiz};
+  float org[3], scl[3];
+  uint32_t qlo[3] = {0, 0, 0}, qhi[3] = {0, 0, 0};
+  for (int k = 0; k < 3; ++k) {
+    float plo = INFINITY, phi = -INFINITY;
+    for (int c = 0; c < 4; ++c)
+      if (g.ref[c] != kEmpty) { plo = std::min(plo, lo[k][c]); phi = std::max(phi, hi[k][c]); }
+    if (!(plo <= phi)) { plo = 0.f; phi = 0.f; }
+    const double ext = (double)phi - (double)plo;
+    double sc = 1.0;
+    if (ext > 0.0) {
+      int e = 0;
+      std::frexp(ext / 255.0, &e);   // ext/255 <= 2^e
+      sc = std::ldexp(1.0, e);
+    }
+    org[k] = plo;
+    scl[k] = (float)sc;
+    for (int c = 0; c < 4; ++c) {
+      uint32_t a = 255u, b = 0u;   // empty interval
+      if (g.ref[c] != kEmpty) {
+        const double fl = std::floor(((double)lo[k][c] - (double)plo) / sc);
+        const double ce = std::ceil(((double)hi[k][c] - (double)plo) / sc);
+        a = (uint32_t)std::min(255.0, std::max(0.0, fl));
+        b = (uint32_t)std::min(255.0, std::max(0.0, ce));
+      }
+      qlo[k] |= a << (8 * c);
+      qhi[k] |= b << (8 * c);
+    }
+  }
+  q.ox = org[0]; q.oy = org[1]; q.oz = org[2];
+  q.sx = scl[0]; q.sy = scl[1]; q.sz = scl[2];
+  q.qlo_x = qlo[0]; q.qhi_x = qhi[0]; q.qlo_y = qlo[1]; q.qhi_y = qhi[1]; q.qlo_z = qlo[2]; q.qhi_z = qhi[2];
+  for (int c = 0; c < 4; ++c) q.ref[c] = g.ref[c];
+  return q;
+}
+
 int validate(const rt_scene_soa* s, const rt_bvh_soa* b) {
   if (!s || !b) return fail(RT_ERR_INVALID, "rt_scene_upload: null scene or bvh");
   if (s->n_vertex_idx % 3 != 0 || s->n_vertex_idx < 0 || s->n_vertices < 0 || s->n_meshes < 0)
@@ -1912,6 +1992,11 @@ int rt_scene_upload_ex(const rt_scene_soa* s, const rt_bvh_soa* b, int device, c
   rc = RT_OK;
   if (rc == RT_OK) rc = upload(&sc->d_nodes, nodes, bytes);
   if (rc == RT_OK) rc = upload(&sc->d_nodes4, nodes4, bytes);
+  if (RT_QNODE && rc == RT_OK) {
+    std::vector<GNode4Q> nodes4q(nodes4.size());
+    for (size_t gi = 0; gi < nodes4.size(); ++gi) nodes4q[gi] = quantise_node(nodes4[gi]);
+    rc = upload(&sc->d_nodes4q, nodes4q, bytes);
+  }
   if (rc == RT_OK) rc = upload(&sc->d_tris, tris, bytes);
   if (rc == RT_OK) rc = upload(&sc->d_slot2dev, slot2dev, bytes);
   if (rc == RT_OK) rc = upload(&sc->d_shade, shade, bytes);
@@ -1963,7 +2048,8 @@ int rt_scene_upload_ex(const rt_scene_soa* s, const rt_bvh_soa* b, int device, c
     const size_t pb = sc->nslots * kFields * sizeof(double);
     const size_t wb = sc->nslots / 64 * 4 * sizeof(unsigned long long);
     const size_t sb = sc->stack_words > kShortStack ? sc->nslots * (size_t)sc->stack_words * sizeof(uint32_t) : 0;
-    if (hipMalloc(reinterpret_cast<void**>(&c.d_ctr), kCtrWords * sizeof(unsigned long long)) != hipSuccess ||
+    if (hipMalloc(reinterpret_cast<void**>(&c.d_ctr), kCtlBytes) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void**>(&c.h_ctl), kCtlBytes, hipHostMallocDefault) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&c.d_pstate), pb) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&c.d_wavelog), wb) != hipSuccess ||
         (sb > 0 && hipMalloc(reinterpret_cast<void**>(&c.d_spill), sb) != hipSuccess) ||
@@ -1972,7 +2058,7 @@ int rt_scene_upload_ex(const rt_scene_soa* s, const rt_bvh_soa* b, int device, c
       rt_scene_free(sc);
       return fail(RT_ERR_HIP, "allocation of launch contexts failed");
     }
-    sc->bytes += (long long)(kCtrWords * sizeof(unsigned long long) + pb + wb + sb);
+    sc->bytes += (long long)(kCtlBytes + pb + wb + sb);
   }
   *out = sc;
   return RT_OK;
@@ -2034,20 +2120,14 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
 
   KParams P;
   std::memset(&P, 0, sizeof P);
-  P.nodes = sc->d_nodes; P.nodes4 = sc->d_nodes4; P.tris = sc->d_tris; P.slot2dev = sc->d_slot2dev; P.shade = sc->d_shade; P.fnorm = sc->d_fnorm;
+  P.nodes = sc->d_nodes; P.nodes4 = sc->d_nodes4; P.nodes4q = sc->d_nodes4q; P.tris = sc->d_tris; P.slot2dev = sc->d_slot2dev; P.shade = sc->d_shade; P.fnorm = sc->d_fnorm;
   P.vnorm = sc->d_vnorm; P.tu = sc->d_tu; P.tv = sc->d_tv; P.texels = sc->d_texels; P.mats = sc->d_mats;
   P.prims = sc->d_prims; P.n_prims = sc->n_prims;
   LaunchCtx& C = sc->ctx[sc->next_ctx];
   const int ci = sc->next_ctx;
   P.ctr = C.d_ctr;
   P.n_frames = n_frames;
-  for (int f = 0; f < n_frames; ++f) {
-    P.out[f] = outs[f];
-    for (int k = 0; k < 3; ++k) {
-      P.cam[f].eye[k] = p[f].camera.eye[k]; P.cam[f].ll[k] = p[f].camera.lower_left[k];
-      P.cam[f].xd[k] = p[f].camera.x_dir[k]; P.cam[f].yd[k] = p[f].camera.y_dir[k];
-    }
-  }
+  P.frames = reinterpret_cast<const FrameDesc*>(reinterpret_cast<unsigned char*>(C.d_ctr) + kCtrBytes);
   P.n_gnodes = sc->n_gnodes;
   P.out_fmt = p->out_format;
   for (int k = 0; k < 3; ++k) {
@@ -2095,8 +2175,22 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   blocks = std::max<long long>(1, std::min<long long>(blocks, (waves_needed + 3) / 4));
   blocks = std::min<long long>(blocks, (long long)(sc->nslots / kBlock));
 
-  if (C.used) HIP_TRY(hipStreamWaitEvent(st, C.ev1, 0));   // previous launch on this context done
-  HIP_TRY(hipMemsetAsync(C.d_ctr, 0, kCtrWords * sizeof(unsigned long long), st));
+  if (C.used) {
+    HIP_TRY(hipStreamWaitEvent(st, C.ev1, 0));   // previous launch on this context done (device side)
+    HIP_TRY(hipEventSynchronize(C.ev1));         // ... and its staged copy consumed (host side)
+  }
+  // zeroed counters + frame table, one copy from the context's pinned staging
+  std::memset(C.h_ctl, 0, kCtrBytes);
+  FrameDesc* fd = reinterpret_cast<FrameDesc*>(C.h_ctl + kCtrBytes);
+  for (int f = 0; f < n_frames; ++f) {
+    std::memset(&fd[f], 0, sizeof(FrameDesc));
+    for (int k = 0; k < 3; ++k) {
+      fd[f].eye[k] = p[f].camera.eye[k]; fd[f].ll[k] = p[f].camera.lower_left[k];
+      fd[f].xd[k] = p[f].camera.x_dir[k]; fd[f].yd[k] = p[f].camera.y_dir[k];
+    }
+    fd[f].out = outs[f];
+  }
+  HIP_TRY(hipMemcpyAsync(C.d_ctr, C.h_ctl, kCtrBytes + (size_t)n_frames * sizeof(FrameDesc), hipMemcpyHostToDevice, st));
   HIP_TRY(hipEventRecord(C.ev0, st));
   if (rows > 0) {
     void* args[] = {&P};
@@ -2307,13 +2401,14 @@ void rt_scene_free(rt_scene* sc) {
   (void)hipSetDevice(sc->device);
   (void)hipDeviceSynchronize();   // launches may still be reading the scene
   void* ptrs[] = {sc->d_nodes, sc->d_nodes4, sc->d_tris, sc->d_shade, sc->d_fnorm, sc->d_vnorm, sc->d_tu,
-                  sc->d_tv, sc->d_texels, sc->d_mats, sc->d_lights, sc->d_slot2dev, sc->d_prims};
+                  sc->d_tv, sc->d_texels, sc->d_mats, sc->d_lights, sc->d_slot2dev, sc->d_prims, sc->d_nodes4q};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   for (LaunchCtx& c : sc->ctx) {
     void* cp[] = {c.d_ctr, c.d_pstate, c.d_spill, c.d_wavelog};
     for (void* q : cp)
       if (q) (void)hipFree(q);
+    if (c.h_ctl) (void)hipHostFree(c.h_ctl);
     if (c.ev0) (void)hipEventDestroy(c.ev0);
     if (c.ev1) (void)hipEventDestroy(c.ev1);
   }

@@ -23,21 +23,30 @@ def max_rows(height, stripe_h, n):
 
 
 class StripeGather:
-    """Pre-allocated gather of per-rank stripe buffers [max_rows, W, C] into [H, W, C] on rank 0."""
+    """Pre-allocated gather of per-rank stripe buffers into whole frames on rank 0.
 
-    def __init__(self, height, width, stripe_h, n, rank, device, dtype=torch.float32, channels=3):
+    frames == 0: buffers are [max_rows, W, C] -> one image [H, W, C].
+    frames == F: buffers are [F, max_rows, W, C] (the F frames of one rt_launch_frames launch)
+    -> [F, H, W, C] with ONE collective per launch instead of F."""
+
+    def __init__(self, height, width, stripe_h, n, rank, device, dtype=torch.float32, channels=3, frames=0):
         self.n, self.rank = n, rank
         self.rows = max_rows(height, stripe_h, n)
         self.ids = [torch.as_tensor(shard_rows(height, stripe_h, n, r), device=device) for r in range(n)]
-        shape = (self.rows, width, channels)
+        lead = (frames,) if frames else ()
+        self.row_dim = 1 if frames else 0
+        shape = lead + (self.rows, width, channels)
         self.gather_list = [torch.empty(shape, dtype=dtype, device=device) for _ in range(n)] if rank == 0 else None
-        self.image = torch.empty((height, width, channels), dtype=dtype, device=device) if rank == 0 else None
+        self.image = torch.empty(lead + (height, width, channels), dtype=dtype, device=device) if rank == 0 else None
 
     def __call__(self, buf):
+        d = self.row_dim
         if self.n == 1:
-            return buf[: self.ids[0].numel()]
+            return buf.narrow(d, 0, self.ids[0].numel())
+        if self.rank == 0 and buf.shape != self.gather_list[0].shape:
+            raise ValueError("buffer shape does not match the gather")
         dist.gather(buf, self.gather_list, dst=0)
         if self.rank == 0:
             for r in range(self.n):
-                self.image.index_copy_(0, self.ids[r], self.gather_list[r][: self.ids[r].numel()])
+                self.image.index_copy_(d, self.ids[r], self.gather_list[r].narrow(d, 0, self.ids[r].numel()))
         return self.image

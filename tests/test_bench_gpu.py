@@ -1,0 +1,40 @@
+"""bench.py end to end on one MI355X (short run): the JSON contract and the frame it renders."""
+import json
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import rtamd
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parents[1]
+
+
+@pytest.fixture(autouse=True)
+def _gpu(gpu_available):
+    return gpu_available
+
+
+@pytest.mark.parametrize("frames", [1, 8])
+def test_bench_json_contract_and_saved_frame(tmp_path, frames):
+    out = tmp_path / "frame.npy"
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--steps", "8", "--warmup", "8", "--width", "320",
+                        "--height", "180", "--frames", str(frames), "--no-cpu-baseline", "--save", str(out)],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 8 and d["value"] > 0
+    assert d["config"]["frames_per_launch"] == frames
+    rf = d["roofline"]
+    assert rf["bound"] == "hbm" and rf["peak"] == 8000.0 and rf["kernel_ms_avg"] > 0
+    hs = rtamd.HostScene.generate("office")
+    hs.prepare()
+    ref, st = rtamd.DeviceScene(hs, 0).render(hs.render_params(320, 180, 1))
+    assert np.array_equal(np.load(out), ref)
+    assert d["config"]["rays_per_frame"] == st.primary_rays + st.shadow_rays + st.reflection_rays

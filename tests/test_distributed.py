@@ -46,6 +46,16 @@ def _worker(rank, world, port, out_dir, stripe_h):
     buf = torch.zeros((g.rows, W, 3), dtype=torch.float64)
     buf[: part.shape[0]] = torch.from_numpy(part)
     img = g(buf)
+    # batched form (one collective for the F frames of a multi-frame launch): frame f = part * (f + 1)
+    F = 3
+    gb = StripeGather(H, W, stripe_h, world, rank, device="cpu", dtype=torch.float64, frames=F)
+    bb = torch.zeros((F, gb.rows, W, 3), dtype=torch.float64)
+    for f in range(F):
+        bb[f, : part.shape[0]] = torch.from_numpy(part) * (f + 1)
+    imgs = gb(bb)
+    if rank == 0:
+        for f in range(F):
+            assert torch.equal(imgs[f], img * (f + 1))
     rays = torch.tensor([cnt.primary_rays + cnt.shadow_rays + cnt.reflection_rays], dtype=torch.float64)
     dist.all_reduce(rays)
     if rank == 0:

@@ -528,17 +528,32 @@ def test_frames_in_one_launch_equal_single_launches(stripes):
     assert not np.array_equal(singles[0], singles[4])   # the cameras really differ
 
 
+def test_many_frames_in_one_launch():
+    import torch
+
+    hs, dev, _ = Case.get("cornell")
+    p = hs.render_params(40, 30, 1)
+    p.out_format = rtamd.RT_OUT_RGB_F64
+    frames = [_moved(p, 0.01 * f) for f in range(rtamd.abi.RT_MAX_FRAMES)]
+    outs = [torch.zeros((30, 40, 3), dtype=torch.float64, device="cuda") for _ in frames]
+    st = dev.launch_frames(frames, [o.data_ptr() for o in outs], stats=True)
+    for f in (0, 17, len(frames) - 1):
+        ref, _ = dev.render(frames[f])
+        assert np.array_equal(outs[f].cpu().numpy(), ref)
+    assert st.primary_rays == 40 * 30 * len(frames)
+
+
 def test_frames_launch_rejects_mismatched_frames():
     import torch
 
     hs, dev, _ = Case.get("cornell")
     p = hs.render_params(32, 24, 1)
-    o = [torch.zeros((24, 32, 3), device="cuda") for _ in range(9)]
+    o = [torch.zeros((24, 32, 3), device="cuda") for _ in range(2)]
     q = rtamd.abi.RenderParams.from_buffer_copy(p)
     q.max_depth = p.max_depth + 1
     with pytest.raises(rtamd.RtError):
         dev.launch_frames([p, q], [o[0].data_ptr(), o[1].data_ptr()])
     with pytest.raises(rtamd.RtError):
-        dev.launch_frames(p, [x.data_ptr() for x in o])          # more than RT_MAX_FRAMES
+        dev.launch_frames(p, [o[0].data_ptr()] * (rtamd.abi.RT_MAX_FRAMES + 1))   # too many frames
     with pytest.raises(rtamd.RtError):
         dev.launch_frames(p, [o[0].data_ptr(), 0])              # null output

@@ -34,7 +34,11 @@ for kind, kw, w, h, spp in CASES:
     spills = dc["stack_spills"]
     diag = (f"  node: simd {dc['node_lanes']/max(1,dc['node_iters']):.1f} lanes, {dc['node_lines']/max(1,dc['node_iters']):.1f} lines"
             f" | leaf: simd {dc['leaf_lanes']/max(1,dc['leaf_iters']):.1f}, {dc['leaf_lines']/max(1,dc['leaf_iters']):.1f} lines"
-            f" | big-leaf tests {dc['big_leaf_tests']/max(1,ws.tri_tests):.2f} | iters/ray node {dc['node_iters']*64/rays:.1f} leaf {dc['leaf_iters']*64/rays:.1f}")
+            f" | big-leaf tests {dc['big_leaf_tests']/max(1,ws.tri_tests):.2f} | iters/ray node {dc['node_iters']*64/rays:.1f} leaf {dc['leaf_iters']*64/rays:.1f}"
+            f"\n     cycles: trav {dc['trav_cycles']/max(1,dc['trav_cycles']+dc['shade_cycles']+dc['fetch_cycles']):.2f}"
+            f" shade {dc['shade_cycles']/max(1,dc['trav_cycles']+dc['shade_cycles']+dc['fetch_cycles']):.2f}"
+            f" fetch {dc['fetch_cycles']/max(1,dc['trav_cycles']+dc['shade_cycles']+dc['fetch_cycles']):.2f}"
+            f" | rounds/ray {dc['trav_rounds']*64/rays:.2f} lanes/round {dc['trav_round_lanes']/max(1,dc['trav_rounds']):.1f}")
     p.flags = rtamd.RT_FLAG_TRAVERSAL_STATS
     _, cs = gpu.render(p)
     m = float(np.median(ms))
