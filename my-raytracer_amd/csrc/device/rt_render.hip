@@ -812,7 +812,8 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
           const D3 r = normalize(sub(scl(s2, hn_), l));
           refl = stdmax(0.0, dot(r, hv_));
         }
-        refl = pow(refl, M.shininess);
+        // pow(+0, y > 0) = +0 exactly: skip the fp64 pow for the (frequent) zero highlight
+        if (!(refl == 0.0 && M.shininess > 0.0)) refl = pow(refl, M.shininess);
         return d3(L6[3] * (hd_.x * diff + M.ks[0] * refl), L6[4] * (hd_.y * diff + M.ks[1] * refl),
                   L6[5] * (hd_.z * diff + M.ks[2] * refl));
       };
@@ -839,8 +840,9 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
         const uint32_t vw = lvis[threadIdx.x];
         for (int j = light; j < batch_end; ++j) {
           const bool occluded = (j == light) ? shadow_hit : (((vw >> j) & 1u) != 0u);
-          const D3 c = contrib_of(j, hp, hn, hview, hdiff, M);
-          if (!occluded) lacc = add(lacc, c);
+          // an occluded light adds colour * 0 * (finite term) = +-0, which leaves the sum (never -0)
+          // unchanged: skip it (the term is finite for any material with finite shininess >= 0)
+          if (!occluded) lacc = add(lacc, contrib_of(j, hp, hn, hview, hdiff, M));
         }
         light = batch_end;
         if (light < P.n_lights) {
