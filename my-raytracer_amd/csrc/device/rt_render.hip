@@ -63,6 +63,13 @@ constexpr int kCtrWords = 32;       // [0,8) work heads, [8,16) stats, [16,32) d
 // deeper entries spill to a per-lane global array.  Bounds LDS per block independently
 // of tree depth, so occupancy stays VGPR-limited.
 constexpr int kShortStack = RT_SHORT_STACK;
+// Top treelet in LDS: the first kTopNodes 4-wide nodes (breadth-first numbering) are copied
+// into each block's LDS; a node iteration whose active lanes all sit in the treelet reads
+// LDS instead of the vector-L1 path.  0 disables.
+#ifndef RT_TOP_NODES
+#define RT_TOP_NODES 64
+#endif
+constexpr int kTopNodes = RT_TOP_NODES > 0 ? RT_TOP_NODES : 1;
 constexpr int kStackMask = kShortStack - 1;
 static_assert((kShortStack & kStackMask) == 0, "RT_SHORT_STACK must be a power of two");
 
@@ -151,7 +158,8 @@ struct KParams {
   size_t nslots;
   int n_gnodes;
   int out_fmt;
-  int pad0[2];
+  int n_top;        // 4-wide nodes cached in LDS (ids [0, n_top))
+  int top_off;      // their LDS byte offset
   double root_lo[3], root_hi[3];
   int W, H;
   int n_lights, max_depth;
@@ -350,6 +358,12 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
   uint32_t* lvis = ltask + kBlock;                                                             // [kBlock]
   uint32_t* stk = lvis + kBlock + threadIdx.x;
   lvis[threadIdx.x] = 0u;
+  if (WIDTH == 4 && P.n_top > 0) {   // top treelet -> LDS (once per persistent block)
+    float4* dst = reinterpret_cast<float4*>(lds_raw + P.top_off);
+    const float4* src = reinterpret_cast<const float4*>(P.nodes4);
+    for (int i = threadIdx.x; i < P.n_top * (int)(sizeof(GNode4) / sizeof(float4)); i += kBlock) dst[i] = src[i];
+    __syncthreads();
+  }
   const int wbase = threadIdx.x & ~63;   // first thread of this wave
   uint32_t* spill = P.spill + (size_t)blockIdx.x * kBlock + threadIdx.x;
 
@@ -703,14 +717,28 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
             const float tz0 = __builtin_fmaf((float)((nqz >> (8 * c)) & 255u), Az, Bz);
             const float tz1 = __builtin_fmaf((float)((fqz >> (8 * c)) & 255u), Az, Bz);
 #else
-          const char* nb = reinterpret_cast<const char*>(P.nodes4) + (size_t)cur * sizeof(GNode4);
-          const float4 nx = *reinterpret_cast<const float4*>(nb + nxo);
-          const float4 fx = *reinterpret_cast<const float4*>(nb + (nxo ^ 16u));
-          const float4 ny = *reinterpret_cast<const float4*>(nb + nyo);
-          const float4 fy = *reinterpret_cast<const float4*>(nb + (nyo ^ 16u));
-          const float4 nz = *reinterpret_cast<const float4*>(nb + nzo);
-          const float4 fz = *reinterpret_cast<const float4*>(nb + (nzo ^ 16u));
-          const uint4 rf = *reinterpret_cast<const uint4*>(nb + 96);
+          float4 nx, fx, ny, fy, nz, fz;
+          uint4 rf;
+          // wave-uniform: every active lane's node is in the LDS treelet -> ds_read, no TD cost
+          if (__ballot(cur >= (uint32_t)P.n_top) == 0) {
+            const unsigned char* lb = lds_raw + P.top_off + cur * (uint32_t)sizeof(GNode4);
+            nx = *reinterpret_cast<const float4*>(lb + nxo);
+            fx = *reinterpret_cast<const float4*>(lb + (nxo ^ 16u));
+            ny = *reinterpret_cast<const float4*>(lb + nyo);
+            fy = *reinterpret_cast<const float4*>(lb + (nyo ^ 16u));
+            nz = *reinterpret_cast<const float4*>(lb + nzo);
+            fz = *reinterpret_cast<const float4*>(lb + (nzo ^ 16u));
+            rf = *reinterpret_cast<const uint4*>(lb + 96);
+          } else {
+            const char* nb = reinterpret_cast<const char*>(P.nodes4) + (size_t)cur * sizeof(GNode4);
+            nx = *reinterpret_cast<const float4*>(nb + nxo);
+            fx = *reinterpret_cast<const float4*>(nb + (nxo ^ 16u));
+            ny = *reinterpret_cast<const float4*>(nb + nyo);
+            fy = *reinterpret_cast<const float4*>(nb + (nyo ^ 16u));
+            nz = *reinterpret_cast<const float4*>(nb + nzo);
+            fz = *reinterpret_cast<const float4*>(nb + (nzo ^ 16u));
+            rf = *reinterpret_cast<const uint4*>(nb + 96);
+          }
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             const float tx0 = __builtin_fmaf(f4c(nx, c), ivx, -oix), tx1 = __builtin_fmaf(f4c(fx, c), ivx, -oix);
@@ -1230,6 +1258,8 @@ size_t lds_bytes(int stack_words) {
   return (size_t)kBlock *
          (7 * sizeof(double) + (2 + (size_t)std::min(stack_words, kShortStack)) * sizeof(uint32_t));
 }
+// ... plus the top treelet (n_top 128-B nodes) after it
+size_t lds_bytes_total(int stack_words, int n_top) { return lds_bytes(stack_words) + (size_t)n_top * sizeof(GNode4); }
 
 }  // namespace
 
@@ -1281,6 +1311,7 @@ struct rt_scene {
   GNode4* d_nodes4 = nullptr;
   GNode4Q* d_nodes4q = nullptr;
   int n_gnodes4 = 0;
+  int n_top = 0;                // 4-wide nodes each block caches in LDS
   std::vector<GMat> mesh_mats;  // host copy: the analytic materials are appended after these
   GPrim* d_prims = nullptr;     // analytic primitives (rt_scene_set_analytic), spheres then planes
   int n_prims = 0;
@@ -1881,19 +1912,37 @@ int rt_scene_upload_ex(const rt_scene_soa* s, const rt_bvh_soa* b, int device, c
       g.ref[1] = g.ref[2] = g.ref[3] = kEmpty;
       nodes4.push_back(g);
     } else {
-      std::vector<int> order;                  // device-tree ids of the collapsed nodes, preorder
+      // Numbering: the first kTopNodes collapsed nodes in breadth-first order (the top
+      // treelet each block caches in LDS), the rest in preorder so a
+      // subtree stays contiguous.  Children always get larger ids than their parent.
+      std::vector<int> order;                  // device-tree ids of the collapsed nodes
       std::vector<Kids> kids;
       std::vector<int> g4(E.left.size(), -1);
-      std::vector<int> stk = {0};
-      while (!stk.empty()) {
-        const int n = stk.back();
-        stk.pop_back();
+      auto assign = [&](int n) {
         g4[n] = (int)order.size();
         order.push_back(n);
         kids.push_back(kids_of(n));
-        const Kids& k = kids.back();
+      };
+      assign(0);
+      for (size_t q = 0; q < order.size() && (int)order.size() < kTopNodes; ++q) {   // breadth-first top
+        const Kids k = kids[q];
+        for (int i = 0; i < k.n && (int)order.size() < kTopNodes; ++i)
+          if (internal(k.c[i])) assign(k.c[i]);
+      }
+      std::vector<int> stk;                    // preorder below the treelet
+      for (int gi = (int)order.size() - 1; gi >= 0; --gi) {
+        const Kids k = kids[gi];
         for (int i = k.n - 1; i >= 0; --i)
-          if (internal(k.c[i])) stk.push_back(k.c[i]);
+          if (internal(k.c[i]) && g4[k.c[i]] < 0) stk.push_back(k.c[i]);
+        while (!stk.empty()) {
+          const int n = stk.back();
+          stk.pop_back();
+          if (g4[n] >= 0) continue;
+          assign(n);
+          const Kids& kn = kids.back();
+          for (int i = kn.n - 1; i >= 0; --i)
+            if (internal(kn.c[i])) stk.push_back(kn.c[i]);
+        }
       }
       nodes4.resize(order.size());
       std::vector<int> need(order.size(), 0);   // stack entries needed below each node
@@ -2020,6 +2069,9 @@ int rt_scene_upload_ex(const rt_scene_soa* s, const rt_bvh_soa* b, int device, c
   sc->depth = depth;
   sc->stack_words = std::max(std::max(1, depth), stack4);
   sc->n_gnodes4 = (int)nodes4.size();
+  sc->n_top = RT_TOP_NODES > 0 ? std::min(kTopNodes, sc->n_gnodes4) : 0;
+  if (const char* e = std::getenv("RT_LDS_TOP"))   // A/B knob: cache fewer nodes (0 = none)
+    sc->n_top = std::max(0, std::min(sc->n_top, std::atoi(e)));
   sc->delta = delta;
   if (nt > 0)
     for (int k = 0; k < 3; ++k) {
@@ -2030,7 +2082,7 @@ int rt_scene_upload_ex(const rt_scene_soa* s, const rt_bvh_soa* b, int device, c
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) { rt_scene_free(sc); return fail(RT_ERR_HIP, "hipGetDeviceProperties failed"); }
   sc->n_cu = prop.multiProcessorCount;
-  const size_t lds = lds_bytes(sc->stack_words);
+  const size_t lds = lds_bytes_total(sc->stack_words, sc->n_top);
   int max_blocks = 1;
   for (int v = 0; v < kNumVariants; ++v) {
     int nb = 0;
@@ -2171,7 +2223,9 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   P.sample_out = sample_out;
 
   const int v = (p->flags & RT_FLAG_TRAVERSAL_STATS) ? 2 : ((p->flags & RT_FLAG_WIDE_STATS) ? 1 : 0);
-  const size_t lds = lds_bytes(sc->stack_words);
+  const size_t lds = lds_bytes_total(sc->stack_words, sc->n_top);
+  P.n_top = sc->n_top;
+  P.top_off = (int)lds_bytes(sc->stack_words);
   const long long waves_needed = (P.n_tiles * 64 + 63) / 64;
   long long blocks = (long long)sc->n_cu * sc->blocks_per_cu[v];
   blocks = std::max<long long>(1, std::min<long long>(blocks, (waves_needed + 3) / 4));
