@@ -223,7 +223,11 @@ int rt_last_kernel_ms(rt_scene* scene, float* ms);
  * traverse / shade / refill cycles (s_memtime), outer iterations, traversal
  * rounds / active lanes (per wave, summed), traversal-stack entries spilled
  * from the LDS ring to global memory, distinct nodes / triangle lines per
- * wave-level node / leaf iteration (summed), triangle tests in leaves of > 4.  Returns the number of words copied. */
+ * wave-level node / leaf iteration (summed), triangle tests in leaves of > 4,
+ * node iterations served from the LDS treelet; word 31 = watchdog flag; words
+ * [32,35) = global-node iterations with one node for the whole wave, distinct
+ * nodes of global-node iterations (summed), leaf iterations with one record.
+ * Returns the number of words copied (at most 40). */
 int rt_debug_counters(rt_scene* scene, unsigned long long* out, int n);
 
 /* Diagnostics: per-wave timeline of the last launch with a STATS flag: words

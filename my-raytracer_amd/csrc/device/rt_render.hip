@@ -49,13 +49,16 @@ using namespace rtk;
 
 namespace {
 
-constexpr int kBlock = 256;
+#ifndef RT_BLOCK
+#define RT_BLOCK 256
+#endif
+constexpr int kBlock = RT_BLOCK;   // threads per persistent block
 constexpr int kGroups = 8;          // work heads (XCD groups)
 #ifndef RT_REFILL
 #define RT_REFILL 16
 #endif
 constexpr int kRefill = RT_REFILL;  // refill a wave when this many lanes are idle
-constexpr int kCtrWords = 32;       // [0,8) work heads, [8,16) stats, [16,32) diagnostics
+constexpr int kCtrWords = 40;       // [0,8) work heads, [8,16) stats, [16,40) diagnostics (31: guard)
 #ifndef RT_SHORT_STACK
 #define RT_SHORT_STACK 16
 #endif
@@ -67,7 +70,7 @@ constexpr int kShortStack = RT_SHORT_STACK;
 // into each block's LDS; a node iteration whose active lanes all sit in the treelet reads
 // LDS instead of the vector-L1 path.  0 disables.
 #ifndef RT_TOP_NODES
-#define RT_TOP_NODES 64
+#define RT_TOP_NODES (RT_BLOCK / 4)   // fills the CU's 160 KB at 16 waves (32 KB of slots per 256 threads)
 #endif
 constexpr int kTopNodes = RT_TOP_NODES > 0 ? RT_TOP_NODES : 1;
 constexpr int kStackMask = kShortStack - 1;
@@ -100,6 +103,14 @@ typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 #define RT_PS_AUX 0   // cache policy bits of path-state accesses (experiment: 2 = nt)
 #endif
 __device__ __forceinline__ double buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+#if defined(RT_EXP_DUP) && (RT_EXP_DUP & 4)
+  {
+    uint32_t v2 = voff;
+    asm volatile("" : "+v"(v2));
+    const auto x = __builtin_amdgcn_raw_buffer_load_b64(r, v2, soff, RT_PS_AUX);
+    asm volatile("" ::"v"(x));
+  }
+#endif
   return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, RT_PS_AUX));
 }
 __device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, double x) {
@@ -123,7 +134,8 @@ enum : int { CS_PRIMARY = 8, CS_SHADOW, CS_REFLECT, CS_NODES, CS_TRIS, CS_HITS, 
 enum : int {
   CD_NODE_ITERS = 16, CD_NODE_LANES, CD_LEAF_ITERS, CD_LEAF_LANES, CD_TRAV_CYCLES, CD_SHADE_CYCLES,
   CD_FETCH_CYCLES, CD_OUTER_ITERS, CD_TRAV_ROUNDS, CD_TRAV_ROUND_LANES, CD_SPILLS, CD_NODE_LINES,
-  CD_LEAF_LINES, CD_BIG_LEAF_TESTS, CD_GUARD = 31   // CD_GUARD: a wave hit the iteration guard
+  CD_LEAF_LINES, CD_BIG_LEAF_TESTS, CD_NODE_LDS_ITERS, CD_GUARD = 31,   // CD_GUARD: a wave hit the iteration guard
+  CD_GNODE_UNIFORM = 32, CD_GNODE_DISTINCT, CD_LEAF_UNIFORM
 };
 constexpr unsigned kGuardIters = 1u << 24;   // persistent-loop watchdog (never reached by a correct kernel)
 
@@ -288,8 +300,49 @@ struct TriOps {
   int mesh;
   uint32_t meta;
 };
-__device__ __forceinline__ TriOps load_tri(const GTri* tris, uint32_t i) {
+// Perturbation experiment (dev builds only): RT_EXP_DUP issues a second, unused copy of
+// one load class (1 global node loads, 2 leaf triangle loads, 4 path-state loads) so its
+// share of the kernel time can be read off the slowdown.  0 in every shipped build.
+#ifndef RT_EXP_DUP
+#define RT_EXP_DUP 0
+#endif
+__device__ __forceinline__ void exp_dup_load(const float4* p) {
+  const float4* q = p;
+  asm volatile("" : "+v"(q));
+  const float4 x = *q;
+  asm volatile("" ::"v"(x.x), "v"(x.y), "v"(x.z), "v"(x.w));
+}
+// Wave-uniform fetches through the scalar cache: when every active lane needs the same
+// node / triangle record, s_load it into SGPRs (address space 4: the scene is read-only for
+// the launch) and skip the vector-L1 data path, whose per-instruction cost binds the
+// kernel.  RT_SCALAR_UNIFORM = 0 disables.
+#ifndef RT_SCALAR_UNIFORM
+#define RT_SCALAR_UNIFORM 1
+#endif
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef double d2v __attribute__((ext_vector_type(2)));
+typedef int i2v __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(4))) const f4v cfloat4;
+typedef __attribute__((address_space(4))) const d2v cdouble2;
+typedef __attribute__((address_space(4))) const i2v cint2;
+__device__ __forceinline__ TriOps load_tri_uniform(const GTri* tris, uint32_t i) {
+  const cdouble2* q = (const cdouble2*)(uintptr_t)(tris) + (size_t)i * 5;
+  const d2v a = q[0], b = q[1], c = q[2], d = q[3], e = q[4];
+  TriOps T;
+  T.e1 = d3(a.x, a.y, b.x);
+  T.e2 = d3(b.y, c.x, c.y);
+  T.p2 = d3(d.x, d.y, e.x);
+  const i2v meta = *((const cint2*)(q + 4) + 1);
+  T.mesh = meta.x;
+  T.meta = (uint32_t)meta.y;
+  return T;
+}
+__device__ __forceinline__ TriOps load_tri(const GTri* tris, uint32_t i, bool dup = false) {
   const double2* q = reinterpret_cast<const double2*>(tris + i);
+  if ((RT_EXP_DUP & 2) && dup) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) exp_dup_load(reinterpret_cast<const float4*>(q) + k);
+  }
   const double2 a = q[0], b = q[1], c = q[2], d = q[3], e = q[4];
   TriOps T;
   T.e1 = d3(a.x, a.y, b.x);
@@ -344,7 +397,7 @@ __device__ __forceinline__ uint32_t u4c(const uint4& v, int c) {
 #endif
 
 template <int WIDTH, bool STATS>
-__global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams P) {
+__global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render_kernel(KParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   double* lds_d = reinterpret_cast<double*>(lds_raw);
   RaySlots R;
@@ -401,7 +454,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
   unsigned long long c_nodes = 0, c_tris = 0;
   unsigned long long d_node_it = 0, d_node_ln = 0, d_leaf_it = 0, d_leaf_ln = 0;
   unsigned long long d_trav = 0, d_shade = 0, d_fetch = 0, d_outer = 0, d_round_it = 0, d_round_ln = 0;
-  unsigned long long d_spills = 0, d_node_lines = 0, d_leaf_lines = 0, d_big_leaf = 0;
+  unsigned long long d_spills = 0, d_node_lines = 0, d_leaf_lines = 0, d_big_leaf = 0, d_node_lds = 0, d_dummy = 0, d_gn_uni = 0, d_gn_dist = 0, d_leaf_uni = 0;
   unsigned long long w_start = STATS ? __builtin_amdgcn_s_memrealtime() : 0ull, w_refill = 0, w_pixels = 0;
   unsigned long long t_stamp = 0;
   auto stamp = [&]() -> unsigned long long { return STATS ? __builtin_amdgcn_s_memtime() : 0ull; };
@@ -605,8 +658,14 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
               c_tris++;
               wave_tick(d_leaf_it, d_leaf_ln, lane);
               wave_distinct((uint32_t)(((unsigned long long)i * sizeof(GTri)) >> 7), d_leaf_lines, lane);
+              const uint32_t i0 = __shfl(i, __ffsll((long long)__ballot(1)) - 1);
+              if (__ballot(i != i0) == 0) wave_tick(d_leaf_uni, d_dummy, lane);
             }
-            const TriOps T = load_tri(P.tris, rec);
+            TriOps T;
+            if (RT_SCALAR_UNIFORM && __ballot(rec != __builtin_amdgcn_readfirstlane(rec)) == 0)
+              T = load_tri_uniform(P.tris, __builtin_amdgcn_readfirstlane(rec));
+            else
+              T = load_tri(P.tris, rec, true);
             const int slot = (int)(T.meta & kSlotMask);
             // Mesh::intersect_triangle (mymesh.cpp:190-215): the same fp64 S, Da, Db, Dt as
             // the CPU (bit-identical operands and operation order).  Division-free early
@@ -721,6 +780,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
           uint4 rf;
           // wave-uniform: every active lane's node is in the LDS treelet -> ds_read, no TD cost
           if (__ballot(cur >= (uint32_t)P.n_top) == 0) {
+            if (STATS) wave_tick(d_node_lds, d_dummy, lane);
             const unsigned char* lb = lds_raw + P.top_off + cur * (uint32_t)sizeof(GNode4);
             nx = *reinterpret_cast<const float4*>(lb + nxo);
             fx = *reinterpret_cast<const float4*>(lb + (nxo ^ 16u));
@@ -729,8 +789,31 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
             nz = *reinterpret_cast<const float4*>(lb + nzo);
             fz = *reinterpret_cast<const float4*>(lb + (nzo ^ 16u));
             rf = *reinterpret_cast<const uint4*>(lb + 96);
+          } else if (RT_SCALAR_UNIFORM && __ballot(cur != __builtin_amdgcn_readfirstlane(cur)) == 0) {
+            // one node for the whole wave: scalar loads, per-lane near/far selection
+            const cfloat4* sn = (const cfloat4*)(uintptr_t)(P.nodes4) +
+                                (size_t)__builtin_amdgcn_readfirstlane(cur) * (sizeof(GNode4) / sizeof(float4));
+            const f4v lx = sn[0], hx = sn[1], ly = sn[2], hy = sn[3], lz = sn[4], hz = sn[5];
+            const f4v r4 = sn[6];
+            const bool px_ = nxo == 0u, py_ = nyo == 32u, pz_ = nzo == 64u;
+            auto sel = [](bool c, const f4v& a, const f4v& b) {
+              return make_float4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
+            };
+            nx = sel(px_, lx, hx); fx = sel(px_, hx, lx);
+            ny = sel(py_, ly, hy); fy = sel(py_, hy, ly);
+            nz = sel(pz_, lz, hz); fz = sel(pz_, hz, lz);
+            rf = make_uint4(__float_as_uint(r4.x), __float_as_uint(r4.y), __float_as_uint(r4.z), __float_as_uint(r4.w));
           } else {
             const char* nb = reinterpret_cast<const char*>(P.nodes4) + (size_t)cur * sizeof(GNode4);
+            if (STATS) {
+              wave_distinct(cur, d_gn_dist, lane);
+              const uint32_t c0 = __shfl(cur, __ffsll((long long)__ballot(1)) - 1);
+              if (__ballot(cur != c0) == 0) wave_tick(d_gn_uni, d_dummy, lane);
+            }
+            if (RT_EXP_DUP & 1) {
+#pragma unroll
+              for (int k = 0; k < 7; ++k) exp_dup_load(reinterpret_cast<const float4*>(nb) + (k == 6 ? 6 : k));
+            }
             nx = *reinterpret_cast<const float4*>(nb + nxo);
             fx = *reinterpret_cast<const float4*>(nb + (nxo ^ 16u));
             ny = *reinterpret_cast<const float4*>(nb + nyo);
@@ -1110,8 +1193,13 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU) render_kernel(KParams
     const unsigned long long a = wave_sum(d_node_it), b = wave_sum(d_node_ln), c = wave_sum(d_leaf_it);
     const unsigned long long d = wave_sum(d_leaf_ln), e = wave_sum(d_round_it), f = wave_sum(d_round_ln);
     const unsigned long long g = wave_sum(d_spills), h = wave_sum(d_node_lines), q = wave_sum(d_leaf_lines);
-    const unsigned long long r = wave_sum(d_big_leaf);
+    const unsigned long long r = wave_sum(d_big_leaf), t = wave_sum(d_node_lds);
+    const unsigned long long gu = wave_sum(d_gn_uni), gd = wave_sum(d_gn_dist), lu = wave_sum(d_leaf_uni);
     if (lane == 0) {
+      atomicAdd(&P.ctr[CD_NODE_LDS_ITERS], t);
+      atomicAdd(&P.ctr[CD_GNODE_UNIFORM], gu);
+      atomicAdd(&P.ctr[CD_GNODE_DISTINCT], gd);
+      atomicAdd(&P.ctr[CD_LEAF_UNIFORM], lu);
       atomicAdd(&P.ctr[CD_NODE_ITERS], a);
       atomicAdd(&P.ctr[CD_NODE_LANES], b);
       atomicAdd(&P.ctr[CD_LEAF_ITERS], c);
@@ -2228,7 +2316,7 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   P.top_off = (int)lds_bytes(sc->stack_words);
   const long long waves_needed = (P.n_tiles * 64 + 63) / 64;
   long long blocks = (long long)sc->n_cu * sc->blocks_per_cu[v];
-  blocks = std::max<long long>(1, std::min<long long>(blocks, (waves_needed + 3) / 4));
+  blocks = std::max<long long>(1, std::min<long long>(blocks, (waves_needed + kBlock / 64 - 1) / (kBlock / 64)));
   blocks = std::min<long long>(blocks, (long long)(sc->nslots / kBlock));
 
   if (C.used) {

@@ -18,7 +18,11 @@ for flags, name in [(rtamd.RT_FLAG_WIDE_STATS, "4-wide"), (rtamd.RT_FLAG_TRAVERS
     rays = st.primary_rays + st.shadow_rays + st.reflection_rays
     tot = d["trav_cycles"] + d["shade_cycles"] + d["fetch_cycles"]
     print(f"{kind} {w}x{h} {name}: rays {rays}  nodes/ray {st.node_visits/rays:.1f} tris/ray {st.tri_tests/rays:.1f}")
-    print(f"  node loop: {d['node_iters']} wave-iters, SIMD eff {d['node_lanes']/(64*max(1,d['node_iters'])):.3f}")
+    print(f"  node loop: {d['node_iters']} wave-iters, SIMD eff {d['node_lanes']/(64*max(1,d['node_iters'])):.3f}, "
+          f"from the LDS treelet {d['node_lds_iters']/max(1,d['node_iters']):.3f}")
+    g = max(1, d['node_iters'] - d['node_lds_iters'])
+    print(f"  global node iters: {g}, one node for the wave {d['gnode_uniform_iters']/g:.3f}, distinct nodes {d['gnode_distinct']/g:.2f}; "
+          f"leaf iters with one record {d['leaf_uniform_iters']/max(1,d['leaf_iters']):.3f}")
     print(f"  leaf loop: {d['leaf_iters']} wave-iters, SIMD eff {d['leaf_lanes']/(64*max(1,d['leaf_iters'])):.3f}")
     print(f"  trav rounds: {d['trav_rounds']}, lanes active {d['trav_round_lanes']/(64*max(1,d['trav_rounds'])):.3f}; outer iters {d['outer_iters']}")
     print(f"  cycles: trav {d['trav_cycles']/tot:.3f} shade {d['shade_cycles']/tot:.3f} fetch {d['fetch_cycles']/tot:.3f} (total wave-cycles {tot:.3e})")

@@ -29,5 +29,6 @@ pass tcc TCC_HIT_sum TCC_MISS_sum
 pass td TD_TD_BUSY_sum
 pass sq1 SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAVES
 pass sq2 SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VMEM_RD
+pass lds SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT
 PMC_CMD="$B" PMC_FRAMES=8 python tools/pmc_summary.py $O/pmc_$TAG.json $O/pmc_${TAG}_*/
 echo "profile $TAG done"
