@@ -478,8 +478,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
     const D3 dir = d3(K.ll[0] + X * K.xd[0] + Y * K.yd[0] - K.eye[0],
                       K.ll[1] + X * K.xd[1] + Y * K.yd[1] - K.eye[1],
                       K.ll[2] + X * K.xd[2] + Y * K.yd[2] - K.eye[2]);
-    ST3(F_SCOL, d3(0, 0, 0));
-    ST(F_W, 1.0);
+    // SCOL = 0 and W = 1 are implicit at depth 0, PCOL = 0 at sample 0 (never stored)
     depth = 0;
     c_primary++;
     emit_ray(d3(K.eye[0], K.eye[1], K.eye[2]), dir, DBL_MAX);
@@ -534,7 +533,6 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
                      ? P.row_begin + lrow
                      : ((lrow / P.stripe_h) * P.stripe_count + P.stripe_index) * P.stripe_h + (lrow % P.stripe_h);
             sample = P.list ? item % P.nsamp : 0;
-            ST3(F_PCOL, d3(0, 0, 0));
             start_sample();
           }
         }
@@ -910,6 +908,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
     want = 0;
     if (state == ST_CLOSEST || state == ST_SHADOW) {
       bool hit_ready = (state == ST_CLOSEST), finish = false;
+      D3 scol = d3(0, 0, 0);   // the sample's colour so far once the path ends (finish)
       D3 hp, hn, hview;
       double mirror = 0.0;
       // lighting() for one light (mytracer.cpp:579-606): Lambert + Phong term of light j
@@ -960,9 +959,10 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
           ST3(F_LACC, lacc);
           launch_batch(hp, mirror);
         } else {   // bounce complete (subtrace, mytracer.cpp:546-555)
-          const double w = LD(F_W);
-          ST3(F_SCOL, add(LD3(F_SCOL), scl(w, scl(1.0 - mirror, lacc))));
+          const double w = depth == 0 ? 1.0 : LD(F_W);
+          scol = add(depth == 0 ? d3(0, 0, 0) : LD3(F_SCOL), scl(w, scl(1.0 - mirror, lacc)));
           if (mirror > 0.0 && depth < P.max_depth) {
+            ST3(F_SCOL, scol);
             ST(F_W, w * mirror);
             depth++;
             if (refl_h >= 0) {   // reflection ray traced by a helper this round
@@ -990,7 +990,8 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
       }
       if (hit_ready) {
         if (best == kNoHit) {   // miss: background (mytracer_gpu.cu:262, :292)
-          ST3(F_SCOL, add(LD3(F_SCOL), scl(LD(F_W), d3(P.bg[0], P.bg[1], P.bg[2]))));
+          const double w = depth == 0 ? 1.0 : LD(F_W);
+          scol = add(depth == 0 ? d3(0, 0, 0) : LD3(F_SCOL), scl(w, d3(P.bg[0], P.bg[1], P.bg[2])));
           finish = true;
         } else {
           if (STATS) c_hits++;
@@ -1056,9 +1057,10 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
             launch_batch(hp, mirror);
           } else {
             for (int j = 0; j < P.n_lights; ++j) lacc = add(lacc, contrib_of(j, hp, hn, hview, hdiff, M));
-            const double w = LD(F_W);
-            ST3(F_SCOL, add(LD3(F_SCOL), scl(w, scl(1.0 - mirror, lacc))));
+            const double w = depth == 0 ? 1.0 : LD(F_W);
+            scol = add(depth == 0 ? d3(0, 0, 0) : LD3(F_SCOL), scl(w, scl(1.0 - mirror, lacc)));
             if (mirror > 0.0 && depth < P.max_depth) {
+              ST3(F_SCOL, scol);
               ST(F_W, w * mirror);
               depth++;
               const D3 d = d3(-hview.x, -hview.y, -hview.z);
@@ -1074,12 +1076,12 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
         }
       }
       if (finish && P.list) {   // adaptive pass: this sample's trace() colour
-        const D3 c = LD3(F_SCOL);
+        const D3 c = scol;
         double* so = P.sample_out + 3 * (size_t)item;
         so[0] = c.x; so[1] = c.y; so[2] = c.z;
         state = heads_left > 0 ? ST_FETCH : ST_DONE;
       } else if (finish) {
-        const D3 pcol = add(LD3(F_PCOL), LD3(F_SCOL));
+        const D3 pcol = add(sample == 0 ? d3(0, 0, 0) : LD3(F_PCOL), scol);
         sample++;
         if (sample < P.spp_n * P.spp_n) {
           ST3(F_PCOL, pcol);
