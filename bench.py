@@ -43,7 +43,7 @@ import torch.distributed as dist
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "my-raytracer_amd"))
 import rtamd  # noqa: E402
-from rtamd.shard import StripeGather, max_rows as shard_max_rows  # noqa: E402
+from rtamd.shard import HaloExchange, StripeGather, max_rows as shard_max_rows  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # The CU's vector-L1 data return (TD): one 64-lane dwordx4 wave-instruction per 16 cycles =
@@ -78,7 +78,7 @@ def parse():
                     help="also trace the scene's spheres/planes (always on for --scene spheres)")
     ap.add_argument("--adaptive", action="store_true",
                     help="each frame = primary pass + adaptive supersampling pass (subp 4, threshold 0.02, "
-                         "mytracer_gpu.cu:83-109); single GPU")
+                         "mytracer_gpu.cu:83-109); N > 1: stripe-edge halo rows exchanged by one all_gather per frame")
     return ap.parse_args()
 
 
@@ -89,8 +89,6 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if a.gpus != world and world > 1:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE {world}")
-    if a.adaptive and world > 1:
-        raise SystemExit("--adaptive needs the full frame on one GPU (neighbour test)")
     n = world
     torch.cuda.set_device(local)
     if n > 1:
@@ -117,7 +115,20 @@ def main():
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(S - 1)]
     buf = bufs[0]
     stream = streams[0].cuda_stream
-    prims = [torch.zeros((a.height, W, 3), dtype=torch.float64, device="cuda") for _ in range(S)] if a.adaptive else []
+    rows_local = rtamd.rows_in_shard(params)
+    prims = [torch.zeros((shard_max_rows(a.height, STRIPE_H, n), W, 3), dtype=torch.float64, device="cuda")
+             for _ in range(S)] if a.adaptive else []
+    # N > 1: the neighbour test of a stripe's edge rows needs the rows the neighbouring ranks
+    # rendered -- ONE all_gather of every rank's stripe-edge rows per frame (rtamd.shard.HaloExchange)
+    halo_x = HaloExchange(a.height, W, STRIPE_H, n, rank, rtamd.adaptive_halo_rows(params), device="cuda") \
+        if a.adaptive and n > 1 else None
+
+    def adaptive_pass(prim, out, stats, stream_):
+        if halo_x is None:
+            return gpu.launch_adaptive(params, prim.data_ptr(), out.data_ptr(), 4, 0.02, stats=stats, stream=stream_)
+        halo = halo_x(prim[:rows_local])
+        return gpu.launch_adaptive_shard(params, prim.data_ptr(), halo.data_ptr(), out.data_ptr(), 4, 0.02,
+                                         stats=stats, stream=stream_)
 
     # ---- counters: canonical rays + algorithmic bytes (untimed launches) ----
     if F > 1:   # same launch shape as the timed ones (identical frames: counts / F are exact)
@@ -138,10 +149,9 @@ def main():
         p64 = rtamd.abi.RenderParams.from_buffer_copy(params)
         p64.out_format = rtamd.RT_OUT_RGB_F64
         gpu.launch(p64, prims[0].data_ptr(), stats=True, stream=stream)
-        ast, nsel = gpu.launch_adaptive(params, prims[0].data_ptr(), buf.data_ptr(), 4, 0.02, stats=True,
-                                        stream=stream)
+        ast, nsel = adaptive_pass(prims[0], buf, True, stream)
         rays_local += ast.primary_rays + ast.shadow_rays + ast.reflection_rays
-        adaptive_info = {"pixels_supersampled": nsel, "subp": 4, "threshold": 0.02,
+        adaptive_info = {("pixels_supersampled" if n == 1 else "pixels_supersampled_rank0"): nsel, "subp": 4, "threshold": 0.02,
                          "rays": ast.primary_rays + ast.shadow_rays + ast.reflection_rays}
     alg_bytes_local = 64 * tst.node_visits + 48 * tst.tri_tests + 64 * tst.closest_hits
     # bytes the production kernel requests from L1: 128-B GNode4, 80-B GTri, 32-B TriShade per hit
@@ -163,8 +173,7 @@ def main():
                 e0.record(s)
             if a.adaptive:
                 gpu.launch(p64, prims[li % S].data_ptr(), stats=False, stream=s.cuda_stream)
-                gpu.launch_adaptive(params, prims[li % S].data_ptr(), bs[0].data_ptr(), 4, 0.02, stats=False,
-                                    stream=s.cuda_stream)
+                adaptive_pass(prims[li % S], bs[0], False, s.cuda_stream)
             elif nf == 1:
                 gpu.launch(params, bs[0].data_ptr(), stats=False, stream=s.cuda_stream)
             else:

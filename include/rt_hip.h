@@ -209,6 +209,25 @@ int rt_launch_frames(rt_scene* scene, const rt_render_params* p, int n_frames, v
 int rt_launch_adaptive(rt_scene* scene, const rt_render_params* p, const double* d_primary, void* d_out, int subp,
                        double threshold, rt_stats* stats, long long* n_selected, void* stream);
 
+/* Adaptive pass over a row shard (the multi-GPU case).  p may use
+ * stripes or a row range; d_primary / d_out are the shard's packed rows (as
+ * rt_launch_compute_image writes them), d_primary in RT_OUT_RGB_F64.  The
+ * neighbour test of a shard's first / last row in each run of consecutive rows
+ * (a stripe, or the row range) needs the primary colour of the row just outside
+ * it: d_halo holds those rows, [segment][2][W][3] doubles, [s][0] = the row
+ * below segment s, [s][1] = the row above it, in the order rt_adaptive_halo_rows
+ * lists them (rows outside the frame are never read; d_halo may be NULL when all
+ * of them are).  Selection and results equal rt_launch_adaptive on the full frame
+ * restricted to the shard's rows. */
+int rt_launch_adaptive_shard(rt_scene* scene, const rt_render_params* p, const double* d_primary,
+                             const double* d_halo, void* d_out, int subp, double threshold, rt_stats* stats,
+                             long long* n_selected, void* stream);
+
+/* Global rows the halo of rt_launch_adaptive_shard must hold: rows_out[2s] = the
+ * row below segment s, rows_out[2s+1] = the row above it, -1 outside the frame.
+ * Returns the entry count (2 x segments); rows_out may be NULL to query it. */
+int rt_adaptive_halo_rows(const rt_render_params* p, int* rows_out, int cap);
+
 /* Convenience for tests / CLI: renders into a HOST buffer (allocates a device
  * buffer internally, synchronous). */
 int rt_render_to_host(rt_scene* scene, const rt_render_params* p, void* host_out, rt_stats* stats);

@@ -182,7 +182,7 @@ struct KParams {
   int tiles_x;
   int pad1;
   long long n_tiles;
-  // list mode (adaptive pass): work item w = one sample (w % nsamp) of the full-frame pixel
+  // list mode (adaptive pass): work item w = one sample (w % nsamp) of the shard's (local) pixel
   // list[w / nsamp]; its trace() colour goes to sample_out[3w..3w+2] (summed in order later)
   const uint32_t* list;
   const unsigned long long* list_count;
@@ -1228,22 +1228,50 @@ __device__ __forceinline__ double nsq3(const double* a, const double* b) {
   return dx * dx + dy * dy + dz * dz;
 }
 
-__global__ void __launch_bounds__(256) adaptive_select_kernel(const double* prim, void* out, int out_fmt, int W,
-                                                              int H, double threshold, int tiles_x, long long n_tiles,
-                                                              uint32_t* list, unsigned long long* count) {
+// Row geometry of a shard for the adaptive neighbour test: local (packed) rows are cut
+// into segments of consecutive global rows (one per stripe, or one row range); the rows
+// just outside a segment come from the halo [segment][0: row below, 1: row above].
+struct ShardRows {
+  int rows, W, H;
+  int row_begin, stripe_h, stripe_count, stripe_index;
+  __host__ __device__ int global_row(int lrow) const {
+    return stripe_count == 1 ? row_begin + lrow
+                             : ((lrow / stripe_h) * stripe_count + stripe_index) * stripe_h + (lrow % stripe_h);
+  }
+  __host__ __device__ int seg_first(int lrow) const { return stripe_count == 1 ? 0 : lrow - lrow % stripe_h; }
+  __host__ __device__ int seg_last(int lrow) const {
+    return stripe_count == 1 ? rows - 1 : min(seg_first(lrow) + stripe_h, rows) - 1;
+  }
+  __host__ __device__ int segment(int lrow) const { return stripe_count == 1 ? 0 : lrow / stripe_h; }
+  __host__ __device__ int segments() const { return stripe_count == 1 ? (rows > 0) : (rows + stripe_h - 1) / stripe_h; }
+};
+
+// adaptive_supersampling_device's selection (mytracer_gpu.cu:170-200) over the shard's
+// rows: normSq differences to the 4 neighbours in the reference order (x+1, y+1, x-1,
+// y-1), interior pixels of the FRAME only; unselected pixels are copied to the output,
+// selected ones are compacted (one atomic per wave) into list as local pixel ids.
+__global__ void __launch_bounds__(256) adaptive_select_kernel(const double* prim, const double* halo, void* out,
+                                                              int out_fmt, ShardRows G, double threshold,
+                                                              int tiles_x, long long n_tiles, uint32_t* list,
+                                                              unsigned long long* count) {
   const long long tile = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int j = threadIdx.x & 63;
+  const int W = G.W;
   bool sel = false;
-  int x = 0, y = 0;
+  int x = 0, lrow = 0;
   if (tile < n_tiles) {
     const long long ty = tile / tiles_x;
     x = (int)(tile - ty * tiles_x) * 8 + (j & 7);
-    y = (int)ty * 8 + (j >> 3);
-    if (x < W && y < H) {
-      const size_t o = 3 * ((size_t)y * W + x);
+    lrow = (int)ty * 8 + (j >> 3);
+    if (x < W && lrow < G.rows) {
+      const size_t o = 3 * ((size_t)lrow * W + x);
       const double* c = prim + o;
-      if (x >= 1 && y >= 1 && x < W - 1 && y < H - 1) {
-        const double n = nsq3(c, c + 3) + nsq3(c, c + 3 * (size_t)W) + nsq3(c, c - 3) + nsq3(c, c - 3 * (size_t)W);
+      const int y = G.global_row(lrow);
+      if (x >= 1 && y >= 1 && x < W - 1 && y < G.H - 1) {
+        const int seg = G.segment(lrow);
+        const double* up = lrow < G.seg_last(lrow) ? c + 3 * (size_t)W : halo + 3 * ((size_t)(2 * seg + 1) * W + x);
+        const double* dn = lrow > G.seg_first(lrow) ? c - 3 * (size_t)W : halo + 3 * ((size_t)(2 * seg) * W + x);
+        const double n = nsq3(c, c + 3) + nsq3(c, up) + nsq3(c, c - 3) + nsq3(c, dn);
         sel = n > threshold;
       }
       if (!sel) {
@@ -1266,7 +1294,7 @@ __global__ void __launch_bounds__(256) adaptive_select_kernel(const double* prim
   base = __shfl(base, leader);
   if (sel) {
     const unsigned long long below = lane == 0 ? 0ull : (m & (~0ull >> (64 - lane)));
-    list[base + __popcll(below)] = (uint32_t)((size_t)y * W + x);
+    list[base + __popcll(below)] = (uint32_t)((size_t)lrow * W + x);
   }
 }
 
@@ -2377,22 +2405,61 @@ int rt_launch_frames(rt_scene* sc, const rt_render_params* p, int n_frames, void
   return launch_render(sc, p, n_frames, d_outs, stats, stream, nullptr, nullptr, 0);
 }
 
-int rt_launch_adaptive(rt_scene* sc, const rt_render_params* p, const double* d_primary, void* d_out, int subp,
-                       double threshold, rt_stats* stats, long long* n_selected, void* stream) {
+namespace {
+ShardRows shard_rows_of(const rt_render_params* p) {
+  ShardRows G;
+  G.W = p->camera.width;
+  G.H = p->camera.height;
+  G.rows = rt_rows_in_shard(p);
+  G.stripe_count = p->stripe_count > 0 ? p->stripe_count : 1;
+  G.stripe_h = p->stripe_height > 0 ? p->stripe_height : 1;
+  G.stripe_index = p->stripe_index;
+  G.row_begin = G.stripe_count == 1 ? std::max(0, p->row_begin) : 0;
+  return G;
+}
+}  // namespace
+
+int rt_adaptive_halo_rows(const rt_render_params* p, int* rows_out, int cap) {
+  if (!p) return fail(RT_ERR_INVALID, "rt_adaptive_halo_rows: null params");
+  const ShardRows G = shard_rows_of(p);
+  const int nseg = G.segments();
+  if (rows_out && cap < 2 * nseg) return fail(RT_ERR_INVALID, "rt_adaptive_halo_rows: buffer too small");
+  for (int sgi = 0; rows_out && sgi < nseg; ++sgi) {
+    const int l0 = G.stripe_count == 1 ? 0 : sgi * G.stripe_h;
+    const int l1 = G.seg_last(l0);
+    const int below = G.global_row(l0) - 1, above = G.global_row(l1) + 1;
+    rows_out[2 * sgi] = below >= 0 ? below : -1;
+    rows_out[2 * sgi + 1] = above < G.H ? above : -1;
+  }
+  return 2 * nseg;
+}
+
+int rt_launch_adaptive_shard(rt_scene* sc, const rt_render_params* p, const double* d_primary, const double* d_halo,
+                             void* d_out, int subp, double threshold, rt_stats* stats, long long* n_selected,
+                             void* stream) {
   if (!sc || !p || !d_primary || !d_out) return fail(RT_ERR_INVALID, "rt_launch_adaptive: null argument");
   if (subp < 1 || subp > 64) return fail(RT_ERR_INVALID, "rt_launch_adaptive: subp must be in [1, 64]");
   const int W = p->camera.width, H = p->camera.height;
   if (W <= 0 || H <= 0) return fail(RT_ERR_INVALID, "bad image size");
-  if ((p->stripe_count > 1) || p->row_begin != 0 || (p->row_end > 0 && p->row_end != H))
-    return fail(RT_ERR_INVALID, "rt_launch_adaptive: needs the full frame (neighbour test), no stripes/row range");
   if (p->out_format != RT_OUT_RGB_F32 && p->out_format != RT_OUT_RGB_F64) return fail(RT_ERR_INVALID, "bad out_format");
+  const int scount = p->stripe_count > 0 ? p->stripe_count : 1;
+  if (p->stripe_index < 0 || p->stripe_index >= scount) return fail(RT_ERR_INVALID, "stripe_index out of range");
+  if (scount > 1 && (p->row_begin != 0 || (p->row_end > 0 && p->row_end != H)))
+    return fail(RT_ERR_INVALID, "row ranges cannot be combined with stripe_count > 1");
+  const ShardRows G = shard_rows_of(p);
+  if (!d_halo) {   // only a shard whose segments border nothing but the frame edge may omit the halo
+    std::vector<int> hr((size_t)std::max(1, 2 * G.segments()));
+    rt_adaptive_halo_rows(p, hr.data(), (int)hr.size());
+    for (int i = 0; i < 2 * G.segments(); ++i)
+      if (hr[(size_t)i] >= 0) return fail(RT_ERR_INVALID, "rt_launch_adaptive_shard: this shard needs halo rows");
+  }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   HIP_TRY(hipSetDevice(sc->device));
   uint32_t* list = nullptr;
   unsigned long long* cnt = nullptr;
   double* samples = nullptr;
   // interior pixels only can be selected
-  const long long cap = (long long)std::max(0, W - 2) * std::max(0, H - 2);
+  const long long cap = (long long)std::max(0, W - 2) * G.rows;
   const int nsamp = subp * subp;
   HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&list), (size_t)std::max(1LL, cap) * sizeof(uint32_t), st));
   HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&cnt), sizeof(unsigned long long), st));
@@ -2400,16 +2467,14 @@ int rt_launch_adaptive(rt_scene* sc, const rt_render_params* p, const double* d_
                          st));
   HIP_TRY(hipMemsetAsync(cnt, 0, sizeof(unsigned long long), st));
   const int tiles_x = (W + 7) / 8;
-  const long long n_tiles = (long long)tiles_x * ((H + 7) / 8);
-  hipLaunchKernelGGL(adaptive_select_kernel, dim3((unsigned)((n_tiles + 3) / 4)), dim3(256), 0, st, d_primary, d_out,
-                     p->out_format, W, H, threshold, tiles_x, n_tiles, list, cnt);
-  HIP_TRY(hipGetLastError());
+  const long long n_tiles = (long long)tiles_x * ((G.rows + 7) / 8);
+  if (n_tiles > 0) {
+    hipLaunchKernelGGL(adaptive_select_kernel, dim3((unsigned)((n_tiles + 3) / 4)), dim3(256), 0, st, d_primary,
+                       d_halo, d_out, p->out_format, G, threshold, tiles_x, n_tiles, list, cnt);
+    HIP_TRY(hipGetLastError());
+  }
   rt_render_params q = *p;
   q.spp_n = subp;
-  q.stripe_count = 1;
-  q.stripe_index = 0;
-  q.row_begin = 0;
-  q.row_end = H;
   int rc = launch_render(sc, &q, 1, &d_out, stats, stream, list, cnt, cap, samples);
   if (rc == RT_OK && cap > 0) {
     hipLaunchKernelGGL(adaptive_reduce_kernel, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, st, list, cnt,
@@ -2428,6 +2493,14 @@ int rt_launch_adaptive(rt_scene* sc, const rt_render_params* p, const double* d_
   return rc;
 }
 
+int rt_launch_adaptive(rt_scene* sc, const rt_render_params* p, const double* d_primary, void* d_out, int subp,
+                       double threshold, rt_stats* stats, long long* n_selected, void* stream) {
+  if (!p) return fail(RT_ERR_INVALID, "rt_launch_adaptive: null argument");
+  const int H = p->camera.height;
+  if ((p->stripe_count > 1) || p->row_begin != 0 || (p->row_end > 0 && p->row_end != H))
+    return fail(RT_ERR_INVALID, "rt_launch_adaptive: needs the full frame (neighbour test), no stripes/row range");
+  return rt_launch_adaptive_shard(sc, p, d_primary, nullptr, d_out, subp, threshold, stats, n_selected, stream);
+}
 
 int rt_render_to_host(rt_scene* sc, const rt_render_params* p, void* host_out, rt_stats* stats) {
   if (!sc || !p || !host_out) return fail(RT_ERR_INVALID, "rt_render_to_host: null argument");

@@ -254,6 +254,20 @@ class DeviceScene:
                    "rt_launch_adaptive")
         return st, int(nsel.value)
 
+    def launch_adaptive_shard(self, params, d_primary, d_halo, d_out, subp=4, threshold=0.02, stats=False,
+                              stream=None):
+        """Adaptive pass over a row shard (rt_launch_adaptive_shard): d_primary / d_out are the
+        shard's packed rows, d_halo the rows adaptive_halo_rows(params) lists (0: none needed)."""
+        st = abi.Stats() if stats else None
+        nsel = C.c_longlong(-1)
+        _check_hip(hip_lib().rt_launch_adaptive_shard(self._h, C.byref(params), C.c_void_p(d_primary),
+                                                      C.c_void_p(d_halo) if d_halo else None, C.c_void_p(d_out),
+                                                      subp, threshold, C.byref(st) if st is not None else None,
+                                                      C.byref(nsel) if stats else None,
+                                                      C.c_void_p(stream) if stream else None),
+                   "rt_launch_adaptive_shard")
+        return st, int(nsel.value)
+
     def render_adaptive(self, params, subp=4, threshold=0.02):
         """Primary pass (fp64) + adaptive pass, the reference's launch_compute_image_device
         (mytracer_gpu.cu:44-113); returns (image[H, W, 3], primary Stats, adaptive Stats, n_selected)."""
@@ -307,6 +321,16 @@ class DeviceScene:
 
 def rows_in_shard(params):
     return int(hip_lib().rt_rows_in_shard(C.byref(params)))
+
+
+def adaptive_halo_rows(params):
+    """Global rows rt_launch_adaptive_shard's halo must hold ([2s] below / [2s+1] above
+    segment s; -1 = outside the frame), from the library itself (no GPU needed)."""
+    n = int(hip_lib().rt_adaptive_halo_rows(C.byref(params), None, 0))
+    _check_hip(min(n, 0), "rt_adaptive_halo_rows")
+    buf = (C.c_int * max(1, n))()
+    _check_hip(min(0, int(hip_lib().rt_adaptive_halo_rows(C.byref(params), buf, n))), "rt_adaptive_halo_rows")
+    return np.array(buf[:n], dtype=np.int64)
 
 
 def shard_rows(height, stripe_height, stripe_count, stripe_index):

@@ -50,3 +50,55 @@ class StripeGather:
             for r in range(self.n):
                 self.image.index_copy_(d, self.ids[r], self.gather_list[r].narrow(d, 0, self.ids[r].numel()))
         return self.image
+
+
+def segments(rows):
+    """Runs of consecutive global rows in a shard's packed row list: [(first, last) local index]."""
+    rows = np.asarray(rows)
+    if rows.size == 0:
+        return []
+    cut = np.flatnonzero(np.diff(rows) != 1) + 1
+    starts = np.concatenate([[0], cut])
+    ends = np.concatenate([cut, [rows.size]]) - 1
+    return list(zip(starts.tolist(), ends.tolist()))
+
+
+class HaloExchange:
+    """Halo rows for the sharded adaptive pass (rt_launch_adaptive_shard).
+
+    The neighbour test of a stripe's first / last row needs the primary colour of the row
+    just below / above it, which another rank rendered.  Every such row is the first or
+    last row of that rank's stripe, so each rank contributes its stripes' edge rows
+    ([2 * segments, W, 3] fp64, padded to the largest rank) to ONE all_gather (RCCL over
+    xGMI with "nccl"; at 1080p / 16-row stripes 136 rows = 6.3 MB in all), then picks its
+    halo [2 * segments, W, 3] out of the gathered edges in the order
+    rt_adaptive_halo_rows lists (halo_rows, from the library).  The only data-path
+    exchange besides the final frame gather."""
+
+    def __init__(self, height, width, stripe_h, n, rank, halo_rows, device, dtype=torch.float64):
+        self.n, self.rank = n, rank
+        self.segs = [segments(shard_rows(height, stripe_h, n, r)) for r in range(n)]
+        self.max_edges = 2 * max(len(s) for s in self.segs)
+        own = self.segs[rank]
+        self.edge_index = torch.tensor([i for a, b in own for i in (a, b)], dtype=torch.long, device=device)
+        where = {}   # global row -> flat index into the gathered edges
+        for r in range(n):
+            rows = shard_rows(height, stripe_h, n, r)
+            for k, (a, b) in enumerate(self.segs[r]):
+                where[int(rows[a])] = r * self.max_edges + 2 * k
+                where[int(rows[b])] = r * self.max_edges + 2 * k + 1
+        missing = [int(y) for y in halo_rows if y >= 0 and int(y) not in where]
+        if missing:
+            raise ValueError(f"halo rows {missing[:4]} are not edge rows of any shard")
+        self.pick = torch.tensor([where.get(int(y), 0) for y in halo_rows], dtype=torch.long, device=device)
+        self.send = torch.zeros((self.max_edges, width, 3), dtype=dtype, device=device)
+        self.recv = [torch.empty_like(self.send) for _ in range(n)]
+
+    def __call__(self, prim):
+        """prim: this rank's packed primary rows [rows, W, 3] (fp64) -> halo [2 * segments, W, 3]."""
+        k = self.edge_index.numel()
+        self.send[:k].copy_(prim.index_select(0, self.edge_index))
+        if self.n == 1:
+            return self.send.index_select(0, self.pick)
+        dist.all_gather(self.recv, self.send)
+        return torch.cat(self.recv, 0).index_select(0, self.pick)

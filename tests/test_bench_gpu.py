@@ -38,3 +38,13 @@ def test_bench_json_contract_and_saved_frame(tmp_path, frames):
     ref, st = rtamd.DeviceScene(hs, 0).render(hs.render_params(320, 180, 1))
     assert np.array_equal(np.load(out), ref)
     assert d["config"]["rays_per_frame"] == st.primary_rays + st.shadow_rays + st.reflection_rays
+
+
+def test_bench_adaptive_pass_runs():
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--steps", "3", "--warmup", "1", "--width", "320",
+                        "--height", "180", "--adaptive", "--no-cpu-baseline"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    ad = d["config"]["adaptive_pass"]
+    assert ad["pixels_supersampled"] > 0 and ad["rays"] > 0 and d["value"] > 0

@@ -351,6 +351,43 @@ def test_adaptive_end_to_end_and_full_frame_only():
         dev.render_adaptive(p)
 
 
+@pytest.mark.parametrize("n,stripe_h", [(2, 16), (3, 8), (4, 1)])
+def test_adaptive_pass_sharded_equals_full_frame(n, stripe_h):
+    # Multi-GPU adaptive pass: every rank runs rt_launch_adaptive_shard on its
+    # stripes with the halo rows its neighbours rendered; the union must equal the full-frame
+    # pass bit for bit (same selection, same samples), ray counts adding up.
+    import torch
+
+    hs, dev, orc = Case.get("office")
+    W, H = 192, 108
+    p = hs.render_params(W, H, 1)
+    p.out_format = rtamd.RT_OUT_RGB_F64
+    prim, _ = orc.render(p)
+    d_prim = torch.from_numpy(prim).cuda()
+    full = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda")
+    st_full, nsel_full = dev.launch_adaptive(p, d_prim.data_ptr(), full.data_ptr(), 4, 0.02, stats=True)
+    assert nsel_full > 0
+    tot_sel, tot = 0, [0, 0, 0]
+    for r in range(n):
+        q = rtamd.abi.RenderParams.from_buffer_copy(p)
+        q.stripe_height, q.stripe_count, q.stripe_index = stripe_h, n, r
+        rows = torch.as_tensor(rtamd.shard_rows(H, stripe_h, n, r), device="cuda")
+        part = d_prim.index_select(0, rows).contiguous()
+        hr = rtamd.adaptive_halo_rows(q)
+        assert len(hr) == 2 * len(np.unique(rtamd.shard_rows(H, stripe_h, n, r) // stripe_h))
+        halo = d_prim.index_select(0, torch.as_tensor(np.where(hr >= 0, hr, 0), device="cuda")).contiguous()
+        out = torch.zeros((rows.numel(), W, 3), dtype=torch.float64, device="cuda")
+        with pytest.raises(rtamd.RtError):   # interior stripes need their halo
+            dev.launch_adaptive_shard(q, part.data_ptr(), 0, out.data_ptr(), 4, 0.02)
+        st, nsel = dev.launch_adaptive_shard(q, part.data_ptr(), halo.data_ptr(), out.data_ptr(), 4, 0.02,
+                                             stats=True)
+        assert torch.equal(out, full.index_select(0, rows))
+        tot_sel += nsel
+        tot = [a + b for a, b in zip(tot, counts(st))]
+    assert tot_sel == nsel_full
+    assert tot == counts(st_full)
+
+
 # ---- analytic primitives (opt-in: DeviceScene(..., analytic=True)) ----
 SPHERE_MAT = "0.05 0.02 0.02  0.7 0.25 0.2  0.6 0.6 0.6  50  0.0  1"
 CHROME_MAT = "0.02 0.02 0.02  0.2 0.2 0.25  0.8 0.8 0.8  80  0.5  1"
