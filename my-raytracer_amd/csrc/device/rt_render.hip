@@ -520,6 +520,9 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
             item = (int)wk;
           } else {
             long long tile = wk >> 6;
+#ifdef RT_EXP_REVERSE   // experiment: fetch each XCD range's tiles in reverse order
+            tile = ((g0 >> 6) + (g1 >> 6) - 1) - tile;
+#endif
             const int j = (int)(wk & 63);
             frame = P.n_frames > 1 ? (int)(tile / P.frame_tiles) : 0;
             tile -= (long long)frame * P.frame_tiles;
