@@ -70,7 +70,7 @@ constexpr int kShortStack = RT_SHORT_STACK;
 // into each block's LDS; a node iteration whose active lanes all sit in the treelet reads
 // LDS instead of the vector-L1 path.  0 disables.
 #ifndef RT_TOP_NODES
-#define RT_TOP_NODES (RT_BLOCK / 4)   // fills the CU's 160 KB at 16 waves (32 KB of slots per 256 threads)
+#define RT_TOP_NODES (RT_BLOCK / 4 - 6)   // fills the CU's 160 KB at 16 waves with the slots and the lights
 #endif
 constexpr int kTopNodes = RT_TOP_NODES > 0 ? RT_TOP_NODES : 1;
 constexpr int kStackMask = kShortStack - 1;
@@ -156,8 +156,7 @@ struct KParams {
   const GTri* tris;
   const uint32_t* slot2dev; // reference slot -> device record (2-wide canonical kernel)
   const TriShade* shade;
-  const double* fnorm;
-  const double* vnorm;
+  const double* tnorm;   // [record][12]: face normal, then the 3 vertex normals (device order)
   const double* tu;
   const double* tv;
   const unsigned char* texels;
@@ -192,7 +191,7 @@ struct KParams {
   const GPrim* prims;
   // frames of this launch (rt_launch_frames): work item w belongs to frame w / (64 * frame_tiles)
   int n_frames;
-  int pad3;
+  int lights_off;           // LDS byte offset of the lights copy ([n_lights][6] doubles)
   long long frame_tiles;
   const FrameDesc* frames;  // [n_frames]
 };
@@ -411,12 +410,15 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
   uint32_t* lvis = ltask + kBlock;                                                             // [kBlock]
   uint32_t* stk = lvis + kBlock + threadIdx.x;
   lvis[threadIdx.x] = 0u;
-  if (WIDTH == 4 && P.n_top > 0) {   // top treelet -> LDS (once per persistent block)
+  // once per persistent block: the top treelet and the lights -> LDS
+  if (WIDTH == 4 && P.n_top > 0) {
     float4* dst = reinterpret_cast<float4*>(lds_raw + P.top_off);
     const float4* src = reinterpret_cast<const float4*>(P.nodes4);
     for (int i = threadIdx.x; i < P.n_top * (int)(sizeof(GNode4) / sizeof(float4)); i += kBlock) dst[i] = src[i];
-    __syncthreads();
   }
+  double* lds_lights = reinterpret_cast<double*>(lds_raw + P.lights_off);
+  for (int i = threadIdx.x; i < P.n_lights * 6; i += kBlock) lds_lights[i] = P.lights[i];
+  __syncthreads();
   const int wbase = threadIdx.x & ~63;   // first thread of this wave
   uint32_t* spill = P.spill + (size_t)blockIdx.x * kBlock + threadIdx.x;
 
@@ -916,7 +918,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
       double mirror = 0.0;
       // lighting() for one light (mytracer.cpp:579-606): Lambert + Phong term of light j
       auto contrib_of = [&](int j, D3 hp_, D3 hn_, D3 hv_, D3 hd_, const GMat& M) {
-        const double* L6 = P.lights + 6 * j;
+        const double* L6 = lds_lights + 6 * j;
         const D3 l = normalize(sub(d3(L6[0], L6[1], L6[2]), hp_));
         const double diff = stdmax(0.0, dot(hn_, l));
         double refl = 0.0;
@@ -932,7 +934,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
       };
       // own shadow ray for light `light`; the rest of the bounce is offered to idle lanes
       auto launch_batch = [&](D3 hp_, double mirror_) {
-        const double* L6 = P.lights + 6 * light;
+        const double* L6 = lds_lights + 6 * light;
         const D3 to_l = sub(d3(L6[0], L6[1], L6[2]), hp_);
         const D3 l = normalize(to_l);
         c_shadow++;
@@ -1014,6 +1016,10 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
             const GMat& Mp = P.mats[mesh];
             hdiff = d3(Mp.kd[0], Mp.kd[1], Mp.kd[2]);
           } else {
+            // the normal record is indexed by the hit record: its loads issue together with the
+            // triangle's (one dependent level fewer than face / vertex-id -> vertex-normal gathers)
+            const double2* nq = reinterpret_cast<const double2*>(P.tnorm + 12 * (size_t)best);
+            const double2 q0 = nq[0], q1 = nq[1], q2 = nq[2], q3 = nq[3], q4 = nq[4], q5 = nq[5];
             const TriOps T = load_tri(P.tris, (uint32_t)best);
             const D3 c4 = sub(ro, T.p2);
             const double S = det3(T.e1, T.e2, c3);
@@ -1022,14 +1028,10 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
             const double gamma = (1.0 - alpha - beta);
             mesh = T.mesh;
             const GMat& Mt = P.mats[mesh];
-            if (Mt.draw_mode == RT_DRAW_FLAT) {
-              const double* fnp = P.fnorm + 3 * (size_t)best;
-              hn = d3(fnp[0], fnp[1], fnp[2]);
-            } else {
-              const TriShade sh = P.shade[best];
-              const double* n0 = P.vnorm + 3 * (size_t)sh.v[0];
-              const double* n1 = P.vnorm + 3 * (size_t)sh.v[1];
-              const double* n2 = P.vnorm + 3 * (size_t)sh.v[2];
+            if (Mt.draw_mode == RT_DRAW_FLAT) {   // normals_[i] (mytracer_gpu.cu:498-500)
+              hn = d3(q0.x, q0.y, q1.x);
+            } else {   // alpha*vn0 + beta*vn1 + gamma*vn2, not renormalised (:501-505)
+              const double n0[3] = {q1.y, q2.x, q2.y}, n1[3] = {q3.x, q3.y, q4.x}, n2[3] = {q4.y, q5.x, q5.y};
               hn = d3(alpha * n0[0] + beta * n1[0] + gamma * n2[0], alpha * n0[1] + beta * n1[1] + gamma * n2[1],
                       alpha * n0[2] + beta * n1[2] + gamma * n2[2]);
             }
@@ -1132,7 +1134,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
             uint32_t tw;
             if (t < n_extra_lights) {
               const int j = light + 1 + t;
-              const double* L6 = P.lights + 6 * j;
+              const double* L6 = lds_lights + 6 * j;
               const D3 to_l = sub(d3(L6[0], L6[1], L6[2]), hp);
               const D3 l = normalize(to_l);
               o = add(hp, scl(1e-4, l));
@@ -1380,7 +1382,9 @@ size_t lds_bytes(int stack_words) {
          (7 * sizeof(double) + (2 + (size_t)std::min(stack_words, kShortStack)) * sizeof(uint32_t));
 }
 // ... plus the top treelet (n_top 128-B nodes) after it
-size_t lds_bytes_total(int stack_words, int n_top) { return lds_bytes(stack_words) + (size_t)n_top * sizeof(GNode4); }
+size_t lds_bytes_total(int stack_words, int n_top) {
+  return lds_bytes(stack_words) + (size_t)n_top * sizeof(GNode4) + RT_MAX_LIGHTS * 6 * sizeof(double);
+}
 
 }  // namespace
 
@@ -1406,8 +1410,7 @@ struct rt_scene {
   GTri* d_tris = nullptr;
   uint32_t* d_slot2dev = nullptr;
   TriShade* d_shade = nullptr;
-  double* d_fnorm = nullptr;
-  double* d_vnorm = nullptr;
+  double* d_tnorm = nullptr;      // [record][12] face + vertex normals
   double* d_tu = nullptr;
   double* d_tv = nullptr;
   unsigned char* d_texels = nullptr;
@@ -2098,7 +2101,7 @@ int rt_scene_upload_ex(const rt_scene_soa* s, const rt_bvh_soa* b, int device, c
     if (E.count[n] > 0) last_dev[(size_t)E.first[n] + E.count[n] - 1] = 1;
   std::vector<GTri> tris((size_t)nt);
   std::vector<TriShade> shade((size_t)nt);
-  std::vector<double> fnorm(3 * (size_t)nt);
+  std::vector<double> tnorm(12 * (size_t)nt);
   std::atomic<bool> bad_uv{false};
   auto fill = [&](long long g0, long long g1) {
   for (long long g = g0; g < g1; ++g) {
@@ -2123,7 +2126,13 @@ int rt_scene_upload_ex(const rt_scene_soa* s, const rt_bvh_soa* b, int device, c
       for (int k = 0; k < 3; ++k)
         if (sh.t[k] < 0 || sh.t[k] >= s->n_tex_coords)
           bad_uv = true;
-    for (int k = 0; k < 3; ++k) fnorm[3 * (size_t)g + k] = s->face_normals[3 * i + k];
+    double* tn = tnorm.data() + 12 * (size_t)g;
+    for (int k = 0; k < 3; ++k) {
+      tn[k] = s->face_normals[3 * i + k];
+      tn[3 + k] = s->vertex_normals[3 * (size_t)v0 + k];
+      tn[6 + k] = s->vertex_normals[3 * (size_t)v1 + k];
+      tn[9 + k] = s->vertex_normals[3 * (size_t)v2 + k];
+    }
   }
   };
   {
@@ -2152,7 +2161,6 @@ int rt_scene_upload_ex(const rt_scene_soa* s, const rt_bvh_soa* b, int device, c
     G.tex_h = s->mesh_tex_height[m];
     G.tex_off = s->mesh_tex_offset[m];
   }
-  std::vector<double> vnorm(s->vertex_normals, s->vertex_normals + 3 * (size_t)s->n_vertices);
   std::vector<double> tu(s->tex_u, s->tex_u + s->n_tex_coords), tv(s->tex_v, s->tex_v + s->n_tex_coords);
   std::vector<unsigned char> texels(s->texels, s->texels + 3 * s->n_texels);
 
@@ -2172,8 +2180,7 @@ int rt_scene_upload_ex(const rt_scene_soa* s, const rt_bvh_soa* b, int device, c
   if (rc == RT_OK) rc = upload(&sc->d_tris, tris, bytes);
   if (rc == RT_OK) rc = upload(&sc->d_slot2dev, slot2dev, bytes);
   if (rc == RT_OK) rc = upload(&sc->d_shade, shade, bytes);
-  if (rc == RT_OK) rc = upload(&sc->d_fnorm, fnorm, bytes);
-  if (rc == RT_OK) rc = upload(&sc->d_vnorm, vnorm, bytes);
+  if (rc == RT_OK) rc = upload(&sc->d_tnorm, tnorm, bytes);
   if (rc == RT_OK) rc = upload(&sc->d_tu, tu, bytes);
   if (rc == RT_OK) rc = upload(&sc->d_tv, tv, bytes);
   if (rc == RT_OK) rc = upload(&sc->d_texels, texels, bytes);
@@ -2295,8 +2302,8 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
 
   KParams P;
   std::memset(&P, 0, sizeof P);
-  P.nodes = sc->d_nodes; P.nodes4 = sc->d_nodes4; P.nodes4q = sc->d_nodes4q; P.tris = sc->d_tris; P.slot2dev = sc->d_slot2dev; P.shade = sc->d_shade; P.fnorm = sc->d_fnorm;
-  P.vnorm = sc->d_vnorm; P.tu = sc->d_tu; P.tv = sc->d_tv; P.texels = sc->d_texels; P.mats = sc->d_mats;
+  P.nodes = sc->d_nodes; P.nodes4 = sc->d_nodes4; P.nodes4q = sc->d_nodes4q; P.tris = sc->d_tris; P.slot2dev = sc->d_slot2dev; P.shade = sc->d_shade; P.tnorm = sc->d_tnorm;
+  P.tu = sc->d_tu; P.tv = sc->d_tv; P.texels = sc->d_texels; P.mats = sc->d_mats;
   P.prims = sc->d_prims; P.n_prims = sc->n_prims;
   LaunchCtx& C = sc->ctx[sc->next_ctx];
   const int ci = sc->next_ctx;
@@ -2347,6 +2354,7 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   const size_t lds = lds_bytes_total(sc->stack_words, sc->n_top);
   P.n_top = sc->n_top;
   P.top_off = (int)lds_bytes(sc->stack_words);
+  P.lights_off = P.top_off + sc->n_top * (int)sizeof(GNode4);
   const long long waves_needed = (P.n_tiles * 64 + 63) / 64;
   long long blocks = (long long)sc->n_cu * sc->blocks_per_cu[v];
   blocks = std::max<long long>(1, std::min<long long>(blocks, (waves_needed + kBlock / 64 - 1) / (kBlock / 64)));
@@ -2622,7 +2630,7 @@ void rt_scene_free(rt_scene* sc) {
   if (!sc) return;
   (void)hipSetDevice(sc->device);
   (void)hipDeviceSynchronize();   // launches may still be reading the scene
-  void* ptrs[] = {sc->d_nodes, sc->d_nodes4, sc->d_tris, sc->d_shade, sc->d_fnorm, sc->d_vnorm, sc->d_tu,
+  void* ptrs[] = {sc->d_nodes, sc->d_nodes4, sc->d_tris, sc->d_shade, sc->d_tnorm, sc->d_tu,
                   sc->d_tv, sc->d_texels, sc->d_mats, sc->d_lights, sc->d_slot2dev, sc->d_prims, sc->d_nodes4q};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
