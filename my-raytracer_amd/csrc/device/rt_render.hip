@@ -1573,7 +1573,10 @@ struct SahData {
   std::vector<std::array<double, 3>> lo, hi, c;   // per reference slot: bounds, centroid
 };
 using V3 = std::array<double, 3>;
-constexpr int kSahBins = 32;
+#ifndef RT_SAH_BINS
+#define RT_SAH_BINS 16   // A/B: 8/16/24 +2 %, 32 baseline, 64/128 -4 % (office); 16 -1 % on random triangles
+#endif
+constexpr int kSahBins = RT_SAH_BINS;   // binned SAH: bins per axis
 const V3 kV3Lo = {DBL_MAX, DBL_MAX, DBL_MAX}, kV3Hi = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
 
 inline void grow3(V3& lo, V3& hi, const V3& l2, const V3& h2) {
