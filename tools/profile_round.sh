@@ -6,7 +6,7 @@ set -e -o pipefail
 TAG=${1:?tag}
 O=gpurun_out
 export TMPDIR=/tmp
-B="python bench.py --no-cpu-baseline"        # default launch shape (32 frames per launch)
+B="python bench.py --no-cpu-baseline"        # default launch shape (64 frames per launch)
 S="python bench.py --steps 5 --warmup 1 --no-cpu-baseline --frames 1"   # one frame per launch
 timeout -k 10 300 python bench.py > $O/bench_$TAG.json 2> $O/bench_$TAG.err
 timeout -k 10 300 python bench.py --steps 32 --warmup 8 --frames 1 --no-cpu-baseline > $O/bench_${TAG}_serial.json 2>> $O/bench_$TAG.err
@@ -30,5 +30,5 @@ pass td TD_TD_BUSY_sum
 pass sq1 SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAVES
 pass sq2 SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VMEM_RD
 pass lds SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT
-PMC_CMD="$B" PMC_FRAMES=32 python tools/pmc_summary.py $O/pmc_$TAG.json $O/pmc_${TAG}_*/
+PMC_CMD="$B" PMC_FRAMES=64 python tools/pmc_summary.py $O/pmc_$TAG.json $O/pmc_${TAG}_*/
 echo "profile $TAG done"

@@ -1,6 +1,6 @@
 """Per-rank launch time of the N-GPU bench, emulated on one GPU (dev tool).
 
-Rank 0's share of N-way row striping (16-row stripes, stripe s -> rank s mod N), max(32, 8 N) frames per
+Rank 0's share of N-way row striping (16-row stripes, stripe s -> rank s mod N), 64 frames per
 launch as bench.py does; prints the launch time and the whole-job rate it implies if every
 rank ran as fast (the gather is not included)."""
 import sys
@@ -17,7 +17,7 @@ host.prepare()
 gpu = rtamd.DeviceScene(host, 0)
 FA = sys.argv[1] if len(sys.argv) > 1 else "auto"
 for n in (1, 2, 4, 8):
-    F = min(64, max(32, 8 * n)) if FA == "auto" else int(FA)
+    F = 64 if FA == "auto" else int(FA)
     p = host.render_params(1920, 1080, 1)
     p.stripe_height, p.stripe_count, p.stripe_index = 16, n, 0
     rows = rtamd.rows_in_shard(p)
