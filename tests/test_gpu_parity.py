@@ -351,6 +351,28 @@ def test_adaptive_end_to_end_and_full_frame_only():
         dev.render_adaptive(p)
 
 
+@pytest.mark.parametrize("kind,w,h", [("cornell", 64, 48), ("office", 96, 54)])
+def test_max_lights(kind, w, h):
+    # RT_MAX_LIGHTS lights: the LDS light table at its largest and shading in several batches
+    # (more shadow rays per bounce than a wave has idle lanes to lend).
+    hs, dev, orc = Case.get(kind)
+    p = hs.render_params(w, h, 1)
+    assert p.n_lights >= 2
+    p.n_lights = rtamd.abi.RT_MAX_LIGHTS
+    for i in range(p.n_lights):
+        a = 2.0 * np.pi * i / p.n_lights
+        src = p.lights[i % 2]
+        for k in range(3):
+            p.lights[i].position[k] = src.position[k] + (0.3 * np.cos(a) if k == 0 else 0.3 * np.sin(a) if k == 2 else 0.0)
+            p.lights[i].color[k] = 0.1 + 0.02 * (i % 5)
+    ref, cnt = orc.render(p, pyoracle.MODE_REFERENCE)
+    p.out_format = rtamd.RT_OUT_RGB_F64
+    img, st = dev.render(p)
+    assert np.abs(img - ref).max() <= TOL64
+    assert counts(st) == [cnt.primary_rays, cnt.shadow_rays, cnt.reflection_rays]
+    assert st.shadow_rays > 8 * st.primary_rays
+
+
 @pytest.mark.parametrize("n,stripe_h", [(2, 16), (3, 8), (4, 1)])
 def test_adaptive_pass_sharded_equals_full_frame(n, stripe_h):
     # Multi-GPU adaptive pass: every rank runs rt_launch_adaptive_shard on its
