@@ -12,8 +12,9 @@ Consecutive frames are rendered --frames at a time (default 64) by ONE launch
 of the persistent kernel (rt_launch_frames: the frames share one work queue,
 so the drain at the end of a launch is paid once per F frames); every frame
 still traces all of its rays.  --streams S > 1 additionally keeps S launches in
-flight on separate streams (default 1: launches serial, so the HIP-event launch
-duration is the kernel's own duration, as rocprofv3 reports it).
+flight on separate streams.  Default: 1 on one GPU (launches serial, so the HIP-event
+launch duration is the kernel's own duration, as rocprofv3 reports it); 2 on N > 1,
+so the RCCL gather of launch i (and the drain of its kernel) overlaps launch i+1.
 
 Rays per frame are the canonical counts returned by the kernel's
 counters in an untimed launch.  Roofline: algorithmic bytes per launch =
@@ -70,8 +71,11 @@ def parse():
                     help="frames per launch (rt_launch_frames, <= 64; default 64): one persistent-kernel "
                          "launch renders F consecutive frames from one work queue, so the per-launch drain is "
                          "paid once per F")
-    ap.add_argument("--streams", type=int, default=1,
-                    help="launches in flight on separate streams (1 = launches strictly serial)")
+    ap.add_argument("--streams", type=int, default=0,
+                    help="launches in flight on separate streams (1 = launches strictly serial; default 1 on "
+                         "one GPU, 2 on N > 1 so the RCCL gather of one launch overlaps the next launch)")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="N > 1: nccl (RCCL over xGMI, the measured path) or gloo (host-staged rehearsal)")
     ap.add_argument("--tree", choices=["sah", "reference"], default="sah",
                     help="device traversal hierarchy (pixels identical either way; DESIGN.md §4)")
     ap.add_argument("--analytic", action="store_true",
@@ -90,23 +94,31 @@ def main():
     if a.gpus != world and world > 1:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE {world}")
     n = world
-    torch.cuda.set_device(local)
+    # rehearsal of the N-rank path on fewer GPUs (dev only): --dist-backend gloo stages the
+    # collectives through host memory and RT_BENCH_DEVICE pins every rank to one device
+    dev = int(os.environ.get("RT_BENCH_DEVICE", local))
+    torch.cuda.set_device(dev)
     if n > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group("gloo")
+    host_staged = a.dist_backend == "gloo"
 
     # ---- host side: scene, normals, SoA, median-split BVH (untimed) ----
     gen = {"n_triangles": a.tris} if a.scene == "random_tris" and a.tris else {}
     host = rtamd.HostScene.generate(a.scene, **gen)
     build_s = host.prepare()
-    gpu = rtamd.DeviceScene(host, device=local, analytic=a.analytic or a.scene == "spheres",
+    gpu = rtamd.DeviceScene(host, device=dev, analytic=a.analytic or a.scene == "spheres",
                              tree=a.tree)
     params = host.render_params(a.width, a.height, a.spp)
     params.stripe_height = STRIPE_H
     params.stripe_count = n
     params.stripe_index = rank
     W = a.width
-    S = max(1, min(a.streams, 8))   # librt_hip keeps 8 launch contexts per scene
+    # librt_hip keeps 8 launch contexts per scene; the halo exchange of --adaptive is single-stream
+    S = 1 if a.adaptive else max(1, min(a.streams or (1 if n == 1 else 2), 8))
     F = 1 if a.adaptive else max(1, min(a.frames or rtamd.abi.RT_MAX_FRAMES, rtamd.abi.RT_MAX_FRAMES))
     # per stream: the F frames of one launch, contiguous, so one collective gathers them
     fbufs = [torch.zeros((F, shard_max_rows(a.height, STRIPE_H, n), W, 3), dtype=torch.float32, device="cuda")
@@ -120,7 +132,8 @@ def main():
              for _ in range(S)] if a.adaptive else []
     # N > 1: the neighbour test of a stripe's edge rows needs the rows the neighbouring ranks
     # rendered -- ONE all_gather of every rank's stripe-edge rows per frame (rtamd.shard.HaloExchange)
-    halo_x = HaloExchange(a.height, W, STRIPE_H, n, rank, rtamd.adaptive_halo_rows(params), device="cuda") \
+    halo_x = HaloExchange(a.height, W, STRIPE_H, n, rank, rtamd.adaptive_halo_rows(params), device="cuda",
+                          host_staged=host_staged) \
         if a.adaptive and n > 1 else None
 
     def adaptive_pass(prim, out, stats, stream_):
@@ -157,7 +170,8 @@ def main():
     # bytes the production kernel requests from L1: 128-B GNode4, 80-B GTri, 96-B normal record per hit
     fetch_bytes_local = 128 * wst.node_visits + 80 * wst.tri_tests + 96 * wst.closest_hits
 
-    gather = StripeGather(a.height, W, STRIPE_H, n, rank, device="cuda", frames=F)
+    gathers = [StripeGather(a.height, W, STRIPE_H, n, rank, device="cuda", frames=F, host_staged=host_staged)
+               for _ in range(S)]
     image = None
 
     starts, ends, launch_frames = [], [], []
@@ -183,7 +197,7 @@ def main():
                 starts.append(e0)
                 ends.append(e1)
                 launch_frames.append(nf)
-            image = gather(fbufs[li % S])   # N>1: ONE RCCL gather of the F frames' stripes + re-interleave
+            image = gathers[li % S](fbufs[li % S])   # N>1: ONE RCCL gather of the F frames' stripes + re-interleave
 
     def run(steps, timed):
         li, done = 0, 0

@@ -29,14 +29,18 @@ class StripeGather:
     frames == F: buffers are [F, max_rows, W, C] (the F frames of one rt_launch_frames launch)
     -> [F, H, W, C] with ONE collective per launch instead of F."""
 
-    def __init__(self, height, width, stripe_h, n, rank, device, dtype=torch.float32, channels=3, frames=0):
+    def __init__(self, height, width, stripe_h, n, rank, device, dtype=torch.float32, channels=3, frames=0,
+                 host_staged=False):
+        """host_staged: device buffers go through host memory (gloo rehearsal of the RCCL path)."""
         self.n, self.rank = n, rank
+        self.host_staged = host_staged
         self.rows = max_rows(height, stripe_h, n)
         self.ids = [torch.as_tensor(shard_rows(height, stripe_h, n, r), device=device) for r in range(n)]
         lead = (frames,) if frames else ()
         self.row_dim = 1 if frames else 0
         shape = lead + (self.rows, width, channels)
-        self.gather_list = [torch.empty(shape, dtype=dtype, device=device) for _ in range(n)] if rank == 0 else None
+        gdev = "cpu" if host_staged else device
+        self.gather_list = [torch.empty(shape, dtype=dtype, device=gdev) for _ in range(n)] if rank == 0 else None
         self.image = torch.empty(lead + (height, width, channels), dtype=dtype, device=device) if rank == 0 else None
 
     def __call__(self, buf):
@@ -45,10 +49,11 @@ class StripeGather:
             return buf.narrow(d, 0, self.ids[0].numel())
         if self.rank == 0 and buf.shape != self.gather_list[0].shape:
             raise ValueError("buffer shape does not match the gather")
-        dist.gather(buf, self.gather_list, dst=0)
+        dist.gather(buf.cpu() if self.host_staged else buf, self.gather_list, dst=0)
         if self.rank == 0:
             for r in range(self.n):
-                self.image.index_copy_(d, self.ids[r], self.gather_list[r].narrow(d, 0, self.ids[r].numel()))
+                part = self.gather_list[r].narrow(d, 0, self.ids[r].numel()).to(self.image.device)
+                self.image.index_copy_(d, self.ids[r], part)
         return self.image
 
 
@@ -75,8 +80,9 @@ class HaloExchange:
     rt_adaptive_halo_rows lists (halo_rows, from the library).  The only data-path
     exchange besides the final frame gather."""
 
-    def __init__(self, height, width, stripe_h, n, rank, halo_rows, device, dtype=torch.float64):
+    def __init__(self, height, width, stripe_h, n, rank, halo_rows, device, dtype=torch.float64, host_staged=False):
         self.n, self.rank = n, rank
+        self.host_staged = host_staged
         self.segs = [segments(shard_rows(height, stripe_h, n, r)) for r in range(n)]
         self.max_edges = 2 * max(len(s) for s in self.segs)
         own = self.segs[rank]
@@ -100,5 +106,9 @@ class HaloExchange:
         self.send[:k].copy_(prim.index_select(0, self.edge_index))
         if self.n == 1:
             return self.send.index_select(0, self.pick)
+        if self.host_staged:   # gloo rehearsal: host copies
+            recv = [t.cpu() for t in self.recv]
+            dist.all_gather(recv, self.send.cpu())
+            return torch.cat(recv, 0).to(self.send.device).index_select(0, self.pick)
         dist.all_gather(self.recv, self.send)
         return torch.cat(self.recv, 0).index_select(0, self.pick)

@@ -48,3 +48,31 @@ def test_bench_adaptive_pass_runs():
     d = json.loads(r.stdout.strip().splitlines()[-1])
     ad = d["config"]["adaptive_pass"]
     assert ad["pixels_supersampled"] > 0 and ad["rays"] > 0 and d["value"] > 0
+
+
+def test_bench_two_ranks_rehearsal(tmp_path):
+    # bench.py's N-rank path (row stripes, frames per launch, two launches in flight, the
+    # per-launch gather and re-interleave) with 2 ranks on this one GPU: gloo stages the
+    # collectives through the host (RCCL refuses two ranks on one device); the assembled frame
+    # must equal the single-GPU render bit for bit.
+    import os
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = tmp_path / "frame2.npy"
+    env = dict(os.environ, RT_BENCH_DEVICE="0")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), str(ROOT / "bench.py"),
+                        "--gpus", "2", "--dist-backend", "gloo", "--steps", "16", "--warmup", "8", "--frames", "8",
+                        "--width", "320", "--height", "180", "--no-cpu-baseline", "--save", str(out)],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["n_gpus"] == 2 and d["config"]["launches_in_flight"] == 2 and d["value"] > 0
+    hs = rtamd.HostScene.generate("office")
+    hs.prepare()
+    ref, st = rtamd.DeviceScene(hs, 0).render(hs.render_params(320, 180, 1))
+    assert np.array_equal(np.load(out), ref)
+    assert d["config"]["rays_per_frame"] == st.primary_rays + st.shadow_rays + st.reflection_rays
