@@ -300,7 +300,8 @@ struct TriOps {
   uint32_t meta;
 };
 // Perturbation experiment (dev builds only): RT_EXP_DUP issues a second, unused copy of
-// one load class (1 global node loads, 2 leaf triangle loads, 4 path-state loads) so its
+// one load class (1 global node loads, 2 leaf triangle loads, 4 path-state loads; 8: the node
+// slab arithmetic instead) so its
 // share of the kernel time can be read off the slowdown.  0 in every shipped build.
 #ifndef RT_EXP_DUP
 #define RT_EXP_DUP 0
@@ -387,6 +388,9 @@ __device__ __forceinline__ uint32_t u4c(const uint4& v, int c) {
 #define RT_QNODE 0   // 1: production traversal on quantised 64-B nodes (0: fp32 128-B nodes)
 #endif
 
+#ifndef RT_EMPTY_BOX
+#define RT_EMPTY_BOX 1   // absent 4-wide children are culled by their empty box, not a ref compare
+#endif
 #ifndef RT_SPECULATIVE
 #define RT_SPECULATIVE 1   // 4-wide: postponed leaves + speculative node traversal
 #endif
@@ -833,8 +837,23 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
 #endif
             const float tn = fmaxf(fmaxf(tx0, ty0), fmaxf(tz0, lo_c));
             const float tf = fminf(fminf(tx1, ty1), fminf(tz1, hi_c));
+#if RT_EXP_DUP & 8   // perturbation: a second, unused copy of the slab arithmetic (VALU sensitivity)
+            {
+              float ivx2 = ivx, ivy2 = ivy, ivz2 = ivz;
+              asm volatile("" : "+v"(ivx2), "+v"(ivy2), "+v"(ivz2));
+              const float a0 = __builtin_fmaf(f4c(nx, c), ivx2, -oix), a1 = __builtin_fmaf(f4c(fx, c), ivx2, -oix);
+              const float b0 = __builtin_fmaf(f4c(ny, c), ivy2, -oiy), b1 = __builtin_fmaf(f4c(fy, c), ivy2, -oiy);
+              const float d0 = __builtin_fmaf(f4c(nz, c), ivz2, -oiz), d1 = __builtin_fmaf(f4c(fz, c), ivz2, -oiz);
+              const float tn2 = fmaxf(fmaxf(a0, b0), fmaxf(d0, lo_c)), tf2 = fminf(fminf(a1, b1), fminf(d1, hi_c));
+              asm volatile("" ::"v"(tn2), "v"(tf2));
+            }
+#endif
             const uint32_t r = u4c(rf, c);
+#if RT_EMPTY_BOX
+            const bool h = tn <= tf;   // absent children carry the empty box [+inf, -inf]
+#else
             const bool h = (tn <= tf) && (r != kEmpty);
+#endif
             k[c] = h ? tn : INFINITY;
             v[c] = r;
             cnt += h ? 1 : 0;
@@ -2031,12 +2050,19 @@ int rt_scene_upload_ex(const rt_scene_soa* s, const rt_bvh_soa* b, int device, c
       g.loz[s_] = round_down_host(E.lo[c][2] - delta);
       g.hiz[s_] = round_up_host(E.hi[c][2] + delta);
     };
+    // an absent child gets the empty box [+inf, -inf]: every slab test misses it, so the
+    // kernel needs no separate "child present" test
+    auto set_empty = [&](GNode4& g, int s_) {
+      g.lox[s_] = g.loy[s_] = g.loz[s_] = INFINITY;
+      g.hix[s_] = g.hiy[s_] = g.hiz[s_] = -INFINITY;
+      g.ref[s_] = kEmpty;
+    };
     if (!internal(0)) {
       GNode4 g;
       std::memset(&g, 0, sizeof g);
       set4(g, 0, 0);
       g.ref[0] = kLeaf | (uint32_t)E.first[0];
-      g.ref[1] = g.ref[2] = g.ref[3] = kEmpty;
+      for (int s_ = 1; s_ < 4; ++s_) set_empty(g, s_);
       nodes4.push_back(g);
     } else {
       // Numbering: the first kTopNodes collapsed nodes in breadth-first order (the top
@@ -2085,7 +2111,7 @@ int rt_scene_upload_ex(const rt_scene_soa* s, const rt_bvh_soa* b, int device, c
             g.ref[s_] = internal(c) ? (uint32_t)g4[c] : (kLeaf | (uint32_t)E.first[c]);
             if (internal(c)) deeper = std::max(deeper, need[g4[c]]);
           } else {
-            g.ref[s_] = kEmpty;
+            set_empty(g, s_);
           }
         }
         need[gi] = k.n - 1 + deeper;
