@@ -76,7 +76,7 @@ def parse():
                          "one GPU, 2 on N > 1 so the RCCL gather of one launch overlaps the next launch)")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="N > 1: nccl (RCCL over xGMI, the measured path) or gloo (host-staged rehearsal)")
-    ap.add_argument("--tree", choices=["sah", "reference"], default="sah",
+    ap.add_argument("--tree", choices=["sah", "sbvh", "reference"], default=os.environ.get("RT_BENCH_TREE", "sbvh"),
                     help="device traversal hierarchy (pixels identical either way; DESIGN.md §4)")
     ap.add_argument("--analytic", action="store_true",
                     help="also trace the scene's spheres/planes (always on for --scene spheres)")
@@ -257,7 +257,8 @@ def main():
                             f"lights={params.n_lights}",
                 "triangles": host.triangle_count,
                 "bvh": f"host: reference median split, depth {host.bvh_depth}; device: "
-                       + ("binned-SAH hierarchy, 4-wide" if a.tree == "sah" else "reference tree refined, 4-wide"),
+                       + {"sah": "binned-SAH hierarchy, 4-wide", "sbvh": "binned SAH with spatial splits, 4-wide",
+                          "reference": "reference tree refined, 4-wide"}[a.tree],
                 "rays_per_frame": int(rays_total),
                 "rays_breakdown_rank0": {"primary": st.primary_rays, "shadow": st.shadow_rays,
                                          "reflection": st.reflection_rays},
@@ -315,7 +316,7 @@ def pmc_traffic(a, n, F):
     shape (profiles/r*/pmc_office1080.json: FETCH_SIZE x 2 (gfx950) + WRITE_SIZE, in bytes,
     production kernel dispatches), or None when this run's shape was not profiled."""
     default = (a.scene == "office" and a.width == 1920 and a.height == 1080 and a.spp == 1 and n == 1
-               and not a.adaptive and a.tree == "sah")
+               and not a.adaptive and a.tree == "sbvh")
     if not default:
         return None
     found = sorted(ROOT.glob("profiles/r*/pmc_office1080.json"))

@@ -145,16 +145,19 @@ int rt_scene_upload(const rt_scene_soa* soa, const rt_bvh_soa* bvh, int device, 
 /* Device traversal hierarchy (never changes a pixel or a ray count: the closest hit is
  * the smallest (t, reference slot) over a conservative superset of candidates, DESIGN.md
  * §4; the canonical counters always walk the reference tree given in `bvh`).
- *   RT_TREE_SAH        binned-SAH tree over all triangles, 4-wide collapsed (default)
+ *   RT_TREE_SBVH       binned SAH with spatial splits (straddling triangles referenced from
+ *                      both sides, clipped bounds), 4-wide collapsed (default); scenes above
+ *                      1 M triangles get RT_TREE_SAH
+ *   RT_TREE_SAH        binned-SAH tree over all triangles (object splits only), 4-wide collapsed
  *   RT_TREE_REFERENCE  the reference median-split tree, oversize leaves refined */
-enum { RT_TREE_SAH = 0, RT_TREE_REFERENCE = 1 };
+enum { RT_TREE_SAH = 0, RT_TREE_REFERENCE = 1, RT_TREE_SBVH = 2 };
 typedef struct rt_upload_options {
   int device_tree;      /* RT_TREE_* */
   int reserved_[7];
 } rt_upload_options;
 
 /* rt_scene_upload with options (NULL = defaults; the environment variable
- * RT_DEVICE_TREE=reference|sah changes the default for A/B runs). */
+ * RT_DEVICE_TREE=reference|sah|sbvh changes the default for A/B runs). */
 int rt_scene_upload_ex(const rt_scene_soa* soa, const rt_bvh_soa* bvh, int device, const rt_upload_options* opt,
                        rt_scene** out);
 

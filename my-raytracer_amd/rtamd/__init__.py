@@ -177,15 +177,15 @@ class DeviceScene:
     def __init__(self, host_scene, device=0, analytic=False, tree=None):
         """analytic=True also uploads the raw scene's spheres and planes (rt_scene_set_analytic,
         CPU intersect_scene semantics); the default traces meshes only, like the reference GPU
-        path (mytracer_gpu.cu:314-328).  tree: None (library default, SAH), "sah" or
-        "reference" -- the device traversal hierarchy (pixels and ray counts do not depend on it)."""
+        path (mytracer_gpu.cu:314-328).  tree: None (library default, "sbvh": SAH with
+        spatial splits), "sbvh", "sah" (object splits only) or "reference" -- the device traversal hierarchy (pixels and ray counts do not depend on it)."""
         self._h = C.c_void_p()
         self.device = device
         if tree is None:
             _check_hip(hip_lib().rt_scene_upload(host_scene.soa, host_scene.bvh, device, C.byref(self._h)),
                        "rt_scene_upload")
         else:
-            kinds = {"sah": abi.RT_TREE_SAH, "reference": abi.RT_TREE_REFERENCE}
+            kinds = {"sah": abi.RT_TREE_SAH, "reference": abi.RT_TREE_REFERENCE, "sbvh": abi.RT_TREE_SBVH}
             if tree not in kinds:
                 raise ValueError(f"tree must be one of {sorted(kinds)}")
             opt = abi.UploadOptions(device_tree=kinds[tree])

@@ -117,7 +117,7 @@ class UploadOptions(C.Structure):
     _fields_ = [("device_tree", C.c_int), ("reserved_", C.c_int * 7)]
 
 
-RT_TREE_SAH, RT_TREE_REFERENCE = 0, 1
+RT_TREE_SAH, RT_TREE_REFERENCE, RT_TREE_SBVH = 0, 1, 2
 
 # Symbols each library must export (declared in include/*.h).
 HIP_SYMBOLS = {

@@ -519,18 +519,25 @@ def test_analytic_bad_arguments_fail_loudly():
                                              ("random_tris", {"n_triangles": 20000}, 160, 90, 1)])
 def test_device_tree_changes_no_pixel(kind, kw, w, h, spp):
     # The closest hit is the smallest (t, reference slot) over a conservative superset of
-    # candidates, so the SAH hierarchy and the refined reference tree give identical bits.
+    # candidates, so the SAH hierarchy, the SAH hierarchy with spatial splits (duplicated,
+    # clipped references) and the refined reference tree give identical bits.
     hs, sah, _ = Case.get(kind, **kw)
     _, ref, _ = Case.get(kind, tree="reference", **kw)
+    _, sbvh, _ = Case.get(kind, tree="sbvh", **kw)
     p = hs.render_params(w, h, spp)
     p.out_format = rtamd.RT_OUT_RGB_F64
     a, sa = sah.render(p)
     b, sb = ref.render(p)
+    c, sc = sbvh.render(p)
     assert np.array_equal(a, b) and counts(sa) == counts(sb)
+    assert np.array_equal(a, c) and counts(sa) == counts(sc)
     p.flags = rtamd.RT_FLAG_WIDE_STATS
     _, wa = sah.render(p)
     _, wb = ref.render(p)
+    _, wc = sbvh.render(p)
     assert wa.node_visits < wb.node_visits   # the point of the option
+    print(f"{kind}: 4-wide node visits / tri tests  sah {wa.node_visits} / {wa.tri_tests}  "
+          f"sbvh {wc.node_visits} / {wc.tri_tests}  reference {wb.node_visits} / {wb.tri_tests}")
 
 
 def test_sah_tree_independent_of_build_threads(monkeypatch):
