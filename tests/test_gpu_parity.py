@@ -540,7 +540,8 @@ def test_device_tree_changes_no_pixel(kind, kw, w, h, spp):
           f"sbvh {wc.node_visits} / {wc.tri_tests}  reference {wb.node_visits} / {wb.tri_tests}")
 
 
-def test_sah_tree_independent_of_build_threads(monkeypatch):
+@pytest.mark.parametrize("tree", ["sah", "sbvh"])
+def test_tree_independent_of_build_threads(monkeypatch, tree):
     hs = rtamd.HostScene.generate("random_tris", n_triangles=300000, seed=5)
     hs.prepare()
     p = hs.render_params(192, 108, 1)
@@ -548,7 +549,7 @@ def test_sah_tree_independent_of_build_threads(monkeypatch):
     out = []
     for t in ("1", "7"):
         monkeypatch.setenv("RT_BUILD_THREADS", t)
-        dev = rtamd.DeviceScene(hs, 0, tree="sah")
+        dev = rtamd.DeviceScene(hs, 0, tree=tree)
         img, st = dev.render(p)
         out.append((img, st.node_visits, st.tri_tests, dev.device_bytes))
         dev.close()
