@@ -521,9 +521,9 @@ def test_device_tree_changes_no_pixel(kind, kw, w, h, spp):
     # The closest hit is the smallest (t, reference slot) over a conservative superset of
     # candidates, so the SAH hierarchy, the SAH hierarchy with spatial splits (duplicated,
     # clipped references) and the refined reference tree give identical bits.
-    hs, sah, _ = Case.get(kind, **kw)
+    hs, sbvh, _ = Case.get(kind, **kw)   # library default: spatial splits
+    _, sah, _ = Case.get(kind, tree="sah", **kw)
     _, ref, _ = Case.get(kind, tree="reference", **kw)
-    _, sbvh, _ = Case.get(kind, tree="sbvh", **kw)
     p = hs.render_params(w, h, spp)
     p.out_format = rtamd.RT_OUT_RGB_F64
     a, sa = sah.render(p)
@@ -624,3 +624,56 @@ def test_frames_launch_rejects_mismatched_frames():
         dev.launch_frames(p, [o[0].data_ptr()] * (rtamd.abi.RT_MAX_FRAMES + 1))   # too many frames
     with pytest.raises(rtamd.RtError):
         dev.launch_frames(p, [o[0].data_ptr(), 0])              # null output
+
+
+# ---- spatial splits: clipped, duplicated references on a hostile scene ----
+def _split_stress_scene(tmp_path):
+    """Long thin fan triangles (the shape spatial splits cut most), two room-sized quads
+    crossing each other and the fan, zero-area triangles (collinear and repeated vertices)
+    and a PHONG strip, with a mirror so reflection rays cross the clipped boxes too."""
+    import math
+    import minirt
+    fan_v, fan_t = [(0.0, 0.0, 0.2)], []
+    n = 120
+    for i in range(n):
+        a = 2 * math.pi * i / n
+        fan_v.append((1.5 * math.cos(a), 0.9 * math.sin(a), 0.2 + 0.3 * math.cos(3 * a)))
+    for i in range(n):
+        fan_t.append((0, 1 + i, 1 + (i + 1) % n))
+    wall_v = [(0.1, -2.0, -2.0), (0.1, 2.0, -2.0), (0.1, 2.0, 2.0), (0.1, -2.0, 2.0),
+              (-2.0, -0.2, -2.0), (2.0, -0.2, -2.0), (2.0, -0.2, 2.0), (-2.0, -0.2, 2.0)]
+    wall_t = [(0, 1, 2), (0, 2, 3), (4, 6, 5), (4, 7, 6)]
+    deg_v = [(-0.5, 0.5, 0.5), (0.0, 0.5, 0.5), (0.5, 0.5, 0.5), (0.3, -0.4, 0.6), (0.3, -0.4, 0.6), (0.9, 0.2, 0.4)]
+    deg_t = [(0, 1, 2), (3, 4, 5), (2, 1, 0)]
+    mirror = ((0.05, 0.05, 0.05), (0.3, 0.3, 0.35), (0.5, 0.5, 0.5), 40.0, 0.4, 1)
+    meshes = [minirt.Mesh(fan_v, fan_t, "FLAT", mirror),
+              minirt.Mesh(wall_v, wall_t, "FLAT", kat_scenes.FLAT_MAT),
+              minirt.Mesh(deg_v, deg_t, "FLAT", kat_scenes.FLAT_MAT)]
+    meshes += kat_scenes.scenes()["phong"][0]
+    lights = [((0.6, 1.4, 3.0), (0.7, 0.7, 0.7)), ((-1.2, -0.3, 2.5), (0.3, 0.35, 0.3))]
+    cam = ((0.35, 0.62, 3.6), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 45.0, 9, 7)
+    path = tmp_path / "split_stress.sce"
+    minirt.write_sce(path, meshes, lights, cam, (0.05, 0.05, 0.1), (0.2, 0.2, 0.2), 3)
+    return path
+
+
+def test_spatial_splits_stress_scene_bit_identical(tmp_path):
+    hs = rtamd.HostScene.load(_split_stress_scene(tmp_path))
+    hs.prepare()
+    p = hs.render_params(96, 72, 2)
+    p.out_format = rtamd.RT_OUT_RGB_F64
+    out = {}
+    for tree in ("sbvh", "sah", "reference"):
+        dev = rtamd.DeviceScene(hs, 0, tree=tree)
+        img, st = dev.render(p)
+        q = rtamd.abi.RenderParams.from_buffer_copy(p)
+        q.flags = rtamd.RT_FLAG_WIDE_STATS
+        _, wst = dev.render(q)
+        out[tree] = (img, counts(st), wst.tri_tests)
+        dev.close()
+    assert np.array_equal(out["sbvh"][0], out["reference"][0]) and out["sbvh"][1] == out["reference"][1]
+    assert np.array_equal(out["sah"][0], out["reference"][0]) and out["sah"][1] == out["reference"][1]
+    assert out["sbvh"][2] < out["sah"][2]   # the fan is split: fewer triangle tests
+    ref, cnt = pyoracle.Oracle(hs.raw, hs).render(p, pyoracle.MODE_REFERENCE)
+    assert np.abs(out["sbvh"][0] - ref).max() <= TOL64
+    assert out["sbvh"][1] == counts(cnt)
