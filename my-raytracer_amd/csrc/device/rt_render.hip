@@ -1851,6 +1851,10 @@ constexpr int kSbvhBins = 32;            // spatial bins per axis
 constexpr int kSbvhBinsMax = 128;        // RT_SBVH_BINS cap
 constexpr double kSbvhAlpha = 1e-5;      // try spatial splits when overlap > alpha * root area
 constexpr double kSbvhBudget = 0.75;     // at most this many extra references per triangle
+// SAH-terminated leaves of up to 2 references (node visit = 1 triangle test): office +3.9 %
+// (15707 -> 16324 Mrays/s, A/B), 4K 16 spp +4.1 %, random triangles -2 %; 3 / 4 references or
+// node costs 0.3 / 2 / 4 lose 0.3-6 %
+constexpr int kSbvhLeafMax = 2;
 
 struct SRef { uint32_t slot; V3 lo, hi; };
 
@@ -1890,6 +1894,8 @@ struct SbvhCtx {
   const rt_scene_soa* s;
   double alpha, root_area;
   int sbins;
+  int leaf_max;      // SAH-terminated leaves of up to this many references (1: always split)
+  double c_trav;     // node visit cost in triangle-test units (leaf termination only)
 };
 
 // Splits the references R of one node (consumed): fills the node box; returns false for a
@@ -2036,6 +2042,10 @@ bool sbvh_split(const SbvhCtx& C, std::vector<SRef>& R, int depth, long long& bu
       }
     }
   }
+  if (n <= C.leaf_max) {   // SAH leaf termination: testing n triangles beats one more level
+    const double a = half_area(lo, hi);
+    if ((double)n * a <= std::min(best_cost, sp_cost) + C.c_trav * a) return false;
+  }
   left.clear();
   right.clear();
   bool done = false;
@@ -2106,16 +2116,13 @@ void sbvh_subtree(const SbvhCtx& C, DevTree& T, int root, std::vector<SRef>&& R,
     jobs.pop_back();
     V3 lo, hi;
     const long long n = (long long)j.refs.size();
-    std::vector<uint32_t> slots;
-    if (n <= kLeafMax)
-      for (const SRef& r : j.refs) slots.push_back(r.slot);
     const bool split = sbvh_split(C, j.refs, j.depth, budget, 1, lo, hi, left, right);
     T.lo[j.id] = lo;
     T.hi[j.id] = hi;
-    if (!split) {
+    if (!split) {   // a leaf leaves the references in place
       T.first[j.id] = (int)records.size();
       T.count[j.id] = (int)n;
-      for (uint32_t q : slots) records.push_back(q);
+      for (const SRef& r : j.refs) records.push_back(r.slot);
       continue;
     }
     const int l = T.add(), r = T.add();
@@ -2158,7 +2165,9 @@ void build_sbvh_tree(const rt_scene_soa* s, DevTree& E, std::vector<uint32_t>& r
     prep(0, nt / threads);
     for (auto& x : th) x.join();
   }
-  SbvhCtx C{s, kSbvhAlpha, 0.0, kSbvhBins};
+  SbvhCtx C{s, kSbvhAlpha, 0.0, kSbvhBins, kSbvhLeafMax, 1.0};
+  if (const char* e = std::getenv("RT_SBVH_LEAF")) C.leaf_max = std::max(1, std::min(8, std::atoi(e)));
+  if (const char* e = std::getenv("RT_SBVH_CTRAV")) C.c_trav = std::atof(e);
   double budget_frac = kSbvhBudget;   // A/B knobs
   if (const char* e = std::getenv("RT_SBVH_ALPHA")) C.alpha = std::atof(e);
   if (const char* e = std::getenv("RT_SBVH_BUDGET")) budget_frac = std::atof(e);

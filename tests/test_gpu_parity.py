@@ -657,14 +657,20 @@ def _split_stress_scene(tmp_path):
     return path
 
 
-def test_spatial_splits_stress_scene_bit_identical(tmp_path):
+def test_spatial_splits_stress_scene_bit_identical(tmp_path, monkeypatch):
     hs = rtamd.HostScene.load(_split_stress_scene(tmp_path))
     hs.prepare()
     p = hs.render_params(96, 72, 2)
     p.out_format = rtamd.RT_OUT_RGB_F64
     out = {}
-    for tree in ("sbvh", "sah", "reference"):
-        dev = rtamd.DeviceScene(hs, 0, tree=tree)
+    for tree in ("sbvh", "sbvh1", "sah", "reference"):
+        # sbvh1: spatial splits with single-reference leaves (RT_SBVH_LEAF=1), so the triangle
+        # test count isolates the effect of the splits from SAH leaf termination
+        if tree == "sbvh1":
+            monkeypatch.setenv("RT_SBVH_LEAF", "1")
+        else:
+            monkeypatch.delenv("RT_SBVH_LEAF", raising=False)
+        dev = rtamd.DeviceScene(hs, 0, tree="sbvh" if tree == "sbvh1" else tree)
         img, st = dev.render(p)
         q = rtamd.abi.RenderParams.from_buffer_copy(p)
         q.flags = rtamd.RT_FLAG_WIDE_STATS
@@ -673,7 +679,8 @@ def test_spatial_splits_stress_scene_bit_identical(tmp_path):
         dev.close()
     assert np.array_equal(out["sbvh"][0], out["reference"][0]) and out["sbvh"][1] == out["reference"][1]
     assert np.array_equal(out["sah"][0], out["reference"][0]) and out["sah"][1] == out["reference"][1]
-    assert out["sbvh"][2] < out["sah"][2]   # the fan is split: fewer triangle tests
+    assert np.array_equal(out["sbvh1"][0], out["reference"][0]) and out["sbvh1"][1] == out["reference"][1]
+    assert out["sbvh1"][2] < out["sah"][2]   # the fan is split: fewer triangle tests
     ref, cnt = pyoracle.Oracle(hs.raw, hs).render(p, pyoracle.MODE_REFERENCE)
     assert np.abs(out["sbvh"][0] - ref).max() <= TOL64
     assert out["sbvh"][1] == counts(cnt)
