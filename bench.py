@@ -8,7 +8,7 @@ One step = one full frame: every rank renders its interleaved 16-row stripes
 (stripe = rank mod N) with one launch of the flattened HIP kernel, then rank 0
 gathers the stripes over RCCL (torch.distributed "nccl") and re-interleaves
 them into the final image.  Total work per step is fixed => "strong" scaling.
-Consecutive frames are rendered --frames at a time (default 64) by ONE launch
+Consecutive frames are rendered --frames at a time (default 128) by ONE launch
 of the persistent kernel (rt_launch_frames: the frames share one work queue,
 so the drain at the end of a launch is paid once per F frames); every frame
 still traces all of its rays.  --streams S > 1 additionally keeps S launches in
@@ -56,8 +56,8 @@ STRIPE_H = 16
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=128)
-    ap.add_argument("--warmup", type=int, default=64)
+    ap.add_argument("--steps", type=int, default=256)
+    ap.add_argument("--warmup", type=int, default=128)
     ap.add_argument("--scene", default="office")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
@@ -68,7 +68,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="cpu_baseline: minimum timed CPU work")
     ap.add_argument("--save", default="", help="rank 0: save the gathered image (.npy)")
     ap.add_argument("--frames", type=int, default=0,
-                    help="frames per launch (rt_launch_frames, <= 64; default 64): one persistent-kernel "
+                    help="frames per launch (rt_launch_frames, <= RT_MAX_FRAMES = 128; default 128): one persistent-kernel "
                          "launch renders F consecutive frames from one work queue, so the per-launch drain is "
                          "paid once per F")
     ap.add_argument("--streams", type=int, default=0,
@@ -119,7 +119,7 @@ def main():
     W = a.width
     # librt_hip keeps 8 launch contexts per scene; the halo exchange of --adaptive is single-stream
     S = 1 if a.adaptive else max(1, min(a.streams or (1 if n == 1 else 2), 8))
-    F = 1 if a.adaptive else max(1, min(a.frames or rtamd.abi.RT_MAX_FRAMES, rtamd.abi.RT_MAX_FRAMES))
+    F = 1 if a.adaptive else max(1, min(a.frames or 128, rtamd.abi.RT_MAX_FRAMES))
     # per stream: the F frames of one launch, contiguous, so one collective gathers them
     fbufs = [torch.zeros((F, shard_max_rows(a.height, STRIPE_H, n), W, 3), dtype=torch.float32, device="cuda")
              for _ in range(S)]

@@ -195,7 +195,7 @@ int rt_launch_compute_image(rt_scene* scene, const rt_render_params* p, void* d_
  * once per batch).  p[f] may differ from p[0] only in camera.eye / lower_left / x_dir /
  * y_dir (an animation path); everything else must be identical.  stats (optional,
  * synchronising) sums the frames.  Results equal n_frames rt_launch_compute_image calls. */
-#define RT_MAX_FRAMES 64
+#define RT_MAX_FRAMES 128
 int rt_launch_frames(rt_scene* scene, const rt_render_params* p, int n_frames, void* const* d_outs,
                      rt_stats* stats, void* stream);
 

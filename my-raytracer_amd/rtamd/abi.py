@@ -12,7 +12,7 @@ RT_ERR_INVALID = -1
 RT_ERR_HIP = -2
 RT_ERR_UNSUPPORTED = -3
 RT_MAX_LIGHTS = 16
-RT_MAX_FRAMES = 64
+RT_MAX_FRAMES = 128
 RT_DRAW_FLAT = 0
 RT_DRAW_PHONG = 1
 RT_OUT_RGB_F32 = 0

@@ -30,5 +30,5 @@ pass td TD_TD_BUSY_sum
 pass sq1 SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAVES
 pass sq2 SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VMEM_RD
 pass lds SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT
-PMC_CMD="$B" PMC_FRAMES=64 python tools/pmc_summary.py $O/pmc_$TAG.json $O/pmc_${TAG}_*/
+PMC_CMD="$B" PMC_FRAMES=128 python tools/pmc_summary.py $O/pmc_$TAG.json $O/pmc_${TAG}_*/
 echo "profile $TAG done"
