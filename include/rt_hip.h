@@ -42,7 +42,11 @@ extern "C" {
 #define RT_ERR_HIP (-2)         /* HIP runtime failure */
 #define RT_ERR_UNSUPPORTED (-3) /* scene exceeds a compiled limit (e.g. BVH depth) */
 
+/* Lights held inline in rt_render_params (and staged in LDS by the kernel).  Scenes with
+ * more lights pass them through rt_render_params.lights_ext (any count up to
+ * RT_LIGHTS_LIMIT); the reference shades any nLights (mytracer_gpu.cu:632). */
 #define RT_MAX_LIGHTS 16
+#define RT_LIGHTS_LIMIT (1 << 20)
 
 /* Host SoA scene: the content of struct Data (mydata.h:28-72) after
  * BVH::initSoA has permuted the per-triangle arrays into leaf order
@@ -105,9 +109,9 @@ enum {
  * mytracer_gpu.cu:158).  stripe_count == 1 renders every row in range. */
 typedef struct rt_render_params {
   rt_camera camera;
-  int n_lights;                          /* <= RT_MAX_LIGHTS */
+  int n_lights;                          /* <= RT_MAX_LIGHTS, or <= RT_LIGHTS_LIMIT with lights_ext */
   int max_depth;                         /* reflection bounces after the primary hit */
-  rt_light lights[RT_MAX_LIGHTS];
+  rt_light lights[RT_MAX_LIGHTS];        /* used when lights_ext == NULL */
   double background[3];
   double ambience[3];
   int spp_n;            /* n: n*n stratified samples per pixel (mytracer_gpu.cu:202-221); 1 = one ray through (x,y) */
@@ -118,7 +122,13 @@ typedef struct rt_render_params {
   int stripe_index;     /* [0, stripe_count) */
   int out_format;       /* RT_OUT_* */
   int flags;            /* RT_FLAG_* */
+  const rt_light* lights_ext;  /* non-NULL: the n_lights lights (host memory, read during the call) */
 } rt_render_params;
+
+/* Light i of a render call (lights_ext when set, else the inline table). */
+static inline const rt_light* rt_params_light(const rt_render_params* p, int i) {
+  return p->lights_ext ? &p->lights_ext[i] : &p->lights[i];
+}
 
 /* Ray counters of one launch (canonical definition: DESIGN.md §5).
  * primary = pixels*spp; shadow = shading points x lights with a shadowable

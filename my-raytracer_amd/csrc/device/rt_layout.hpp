@@ -52,19 +52,6 @@ struct alignas(128) GNode4 {
 };
 static_assert(sizeof(GNode4) == 128, "GNode4 must be 128 bytes");
 
-// Quantised 4-wide node (64 B = 4 x dwordx4; build option RT_QNODE): the same children as
-// GNode4 with their fp32 boxes re-expressed on an 8-bit grid anchored at the union box's low
-// corner: plane = origin + q * scale (scale a power of two), q rounded outward (lo down, hi
-// up), so every decoded box contains the fp32 box.  Absent children: qlo = 255, qhi = 0.
-struct alignas(64) GNode4Q {
-  float ox, oy, oz, sx;            // origin, scale x
-  float sy, sz;                    // scale y, z
-  uint32_t qlo_x, qhi_x;           // byte c = child c
-  uint32_t qlo_y, qhi_y, qlo_z, qhi_z;
-  uint32_t ref[4];
-};
-static_assert(sizeof(GNode4Q) == 64, "GNode4Q must be 64 bytes");
-
 // GTri.meta: reference leaf slot (the tie-break key and the 2-wide iteration
 // order) plus two end-of-leaf flags.  Records sit in DEVICE order: the reference
 // leaf order, except that oversize reference leaves are refined into sub-leaves

@@ -82,11 +82,12 @@ static_assert((kShortStack & kStackMask) == 0, "RT_SHORT_STACK must be a power o
 // owner of the same wave for one round (HSHADOW / HCLOSEST): they trace one of its
 // extra shadow rays or its reflection ray, so a bounce costs one round, not 1 + lights.
 enum : int { ST_FETCH = 0, ST_CLOSEST = 1, ST_SHADOW = 2, ST_DONE = 3, ST_HSHADOW = 4, ST_HCLOSEST = 5 };
-#ifndef RT_FANOUT
-#define RT_FANOUT 2   // 0: off, 1: extra shadow rays, 2: + reflection ray
-#endif
 constexpr uint32_t kTaskNone = 0xffffffffu;
-constexpr uint32_t kTaskRefl = 0x10000u;   // task word: owner lane | light << 8 | kTaskRefl
+// task word: owner lane | (light - owner's first light of the batch) << 8, or owner lane | kTaskRefl
+constexpr uint32_t kTaskRefl = 0x10000u;
+// a bounce's shadow rays go out in batches of at most 1 + kBatchExtra lights (the owner's
+// own ray + one helper per extra light): the helpers' occlusion bits fit one LDS word
+constexpr int kBatchExtra = 31;
 
 // Orders LDS traffic between lanes of one wave: LDS executes a wave's operations in
 // issue order, so it suffices to stop the compiler from moving memory operations
@@ -100,22 +101,11 @@ __device__ __forceinline__ void wave_lds_sync() {
 // Raw buffer access (gfx9 resource word 3; no format conversion).
 constexpr int kBufWord3 = 0x00020000;
 typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
-#ifndef RT_PS_AUX
-#define RT_PS_AUX 0   // cache policy bits of path-state accesses (experiment: 2 = nt)
-#endif
 __device__ __forceinline__ double buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-#if defined(RT_EXP_DUP) && (RT_EXP_DUP & 4)
-  {
-    uint32_t v2 = voff;
-    asm volatile("" : "+v"(v2));
-    const auto x = __builtin_amdgcn_raw_buffer_load_b64(r, v2, soff, RT_PS_AUX);
-    asm volatile("" ::"v"(x));
-  }
-#endif
-  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, RT_PS_AUX));
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
 }
 __device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, double x) {
-  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, x), r, voff, soff, RT_PS_AUX);
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, x), r, voff, soff, 0);
 }
 
 
@@ -138,7 +128,12 @@ enum : int {
   CD_LEAF_LINES, CD_BIG_LEAF_TESTS, CD_NODE_LDS_ITERS, CD_GUARD = 31,   // CD_GUARD: a wave hit the iteration guard
   CD_GNODE_UNIFORM = 32, CD_GNODE_DISTINCT, CD_LEAF_UNIFORM
 };
-constexpr unsigned kGuardIters = 1u << 24;   // persistent-loop watchdog (never reached by a correct kernel)
+// Watchdogs (never reached by a correct kernel): the persistent loop, and the wave-level
+// iterations of one traversal round (round, node and leaf loops together).  A wave that
+// trips either ends its work instead of spinning and flags the launch (CD_GUARD), which
+// the host reports as an error.
+constexpr unsigned kGuardIters = 1u << 24;
+constexpr unsigned kTravGuard = 1u << 24;
 
 constexpr int kMaxFrames = RT_MAX_FRAMES;   // frames per launch
 // per-frame camera and output buffer; a launch's table follows its counters in device memory
@@ -153,7 +148,6 @@ constexpr size_t kCtlBytes = kCtrBytes + kMaxFrames * sizeof(FrameDesc);
 struct KParams {
   const GNode* nodes;
   const GNode4* nodes4;
-  const GNode4Q* nodes4q;   // RT_QNODE builds only
   const GTri* tris;
   const uint32_t* slot2dev; // reference slot -> device record (2-wide canonical kernel)
   const TriShade* shade;
@@ -300,50 +294,8 @@ struct TriOps {
   int mesh;
   uint32_t meta;
 };
-// Perturbation experiment (dev builds only): RT_EXP_DUP issues a second, unused copy of
-// one load class (1 global node loads, 2 leaf triangle loads, 4 path-state loads; 8: the node
-// slab arithmetic instead) so its
-// share of the kernel time can be read off the slowdown.  0 in every shipped build.
-#ifndef RT_EXP_DUP
-#define RT_EXP_DUP 0
-#endif
-__device__ __forceinline__ void exp_dup_load(const float4* p) {
-  const float4* q = p;
-  asm volatile("" : "+v"(q));
-  const float4 x = *q;
-  asm volatile("" ::"v"(x.x), "v"(x.y), "v"(x.z), "v"(x.w));
-}
-// Wave-uniform fetches through the scalar cache: when every active lane needs the same
-// node / triangle record, s_load it into SGPRs (address space 4: the scene is read-only for
-// the launch) and skip the vector-L1 data path, whose per-instruction cost binds the
-// kernel.  RT_SCALAR_UNIFORM = 0 disables.
-#ifndef RT_SCALAR_UNIFORM
-#define RT_SCALAR_UNIFORM 0   // off: +0.7 % only, and two differently scheduled builds with it hung
-#endif
-typedef float f4v __attribute__((ext_vector_type(4)));
-typedef double d2v __attribute__((ext_vector_type(2)));
-typedef int i2v __attribute__((ext_vector_type(2)));
-typedef __attribute__((address_space(4))) const f4v cfloat4;
-typedef __attribute__((address_space(4))) const d2v cdouble2;
-typedef __attribute__((address_space(4))) const i2v cint2;
-__device__ __forceinline__ TriOps load_tri_uniform(const GTri* tris, uint32_t i) {
-  const cdouble2* q = (const cdouble2*)(uintptr_t)(tris) + (size_t)i * 5;
-  const d2v a = q[0], b = q[1], c = q[2], d = q[3], e = q[4];
-  TriOps T;
-  T.e1 = d3(a.x, a.y, b.x);
-  T.e2 = d3(b.y, c.x, c.y);
-  T.p2 = d3(d.x, d.y, e.x);
-  const i2v meta = *((const cint2*)(q + 4) + 1);
-  T.mesh = meta.x;
-  T.meta = (uint32_t)meta.y;
-  return T;
-}
-__device__ __forceinline__ TriOps load_tri(const GTri* tris, uint32_t i, bool dup = false) {
+__device__ __forceinline__ TriOps load_tri(const GTri* tris, uint32_t i) {
   const double2* q = reinterpret_cast<const double2*>(tris + i);
-  if ((RT_EXP_DUP & 2) && dup) {
-#pragma unroll
-    for (int k = 0; k < 5; ++k) exp_dup_load(reinterpret_cast<const float4*>(q) + k);
-  }
   const double2 a = q[0], b = q[1], c = q[2], d = q[3], e = q[4];
   TriOps T;
   T.e1 = d3(a.x, a.y, b.x);
@@ -385,17 +337,6 @@ __device__ __forceinline__ uint32_t u4c(const uint4& v, int c) {
   return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
 }
 
-#ifndef RT_QNODE
-#define RT_QNODE 0   // 1: production traversal on quantised 64-B nodes (0: fp32 128-B nodes)
-#endif
-
-#ifndef RT_EMPTY_BOX
-#define RT_EMPTY_BOX 1   // absent 4-wide children are culled by their empty box, not a ref compare
-#endif
-#ifndef RT_SPECULATIVE
-#define RT_SPECULATIVE 1   // 4-wide: postponed leaves + speculative node traversal
-#endif
-
 #ifndef RT_WAVES_PER_EU
 #define RT_WAVES_PER_EU 4   // 4 waves/SIMD = 16 waves/CU (register budget 128 VGPRs)
 #endif
@@ -421,8 +362,11 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
     const float4* src = reinterpret_cast<const float4*>(P.nodes4);
     for (int i = threadIdx.x; i < P.n_top * (int)(sizeof(GNode4) / sizeof(float4)); i += kBlock) dst[i] = src[i];
   }
+  // lights: staged in LDS when the table fits (RT_MAX_LIGHTS), else read from global memory
   double* lds_lights = reinterpret_cast<double*>(lds_raw + P.lights_off);
-  for (int i = threadIdx.x; i < P.n_lights * 6; i += kBlock) lds_lights[i] = P.lights[i];
+  const bool lights_lds = P.n_lights <= RT_MAX_LIGHTS;
+  if (lights_lds)
+    for (int i = threadIdx.x; i < P.n_lights * 6; i += kBlock) lds_lights[i] = P.lights[i];
   __syncthreads();
   const int wbase = threadIdx.x & ~63;   // first thread of this wave
   uint32_t* spill = P.spill + (size_t)blockIdx.x * kBlock + threadIdx.x;
@@ -448,7 +392,8 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
 
   // ---- per-lane state live across phases ----
   int state = ST_FETCH;
-  int px = 0, lrow = 0, py = 0, sample = 0, depth = 0, light = 0, mesh = 0, item = 0, frame = 0;
+  int px = 0, lrow = 0, py = 0, sample = 0, depth = 0, light = 0, mesh = 0, frame = 0;
+  long long item = 0;       // list mode: work item (pixel * nsamp + sample), may exceed 2^31
   int best = kNoHit;        // device record of the closest hit
   int best_slot = kNoHit;   // its reference slot (tie-break key)
   double thit = DBL_MAX;
@@ -465,6 +410,13 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
   unsigned long long w_start = STATS ? __builtin_amdgcn_s_memrealtime() : 0ull, w_refill = 0, w_pixels = 0;
   unsigned long long t_stamp = 0;
   auto stamp = [&]() -> unsigned long long { return STATS ? __builtin_amdgcn_s_memtime() : 0ull; };
+
+  // light j: position xyz, colour rgb (the branch is wave-uniform)
+  struct Light6 { D3 pos, col; };
+  auto light_of = [&](int j) -> Light6 {
+    const double* L = lights_lds ? lds_lights + 6 * j : P.lights + 6 * (size_t)j;
+    return Light6{d3(L[0], L[1], L[2]), d3(L[3], L[4], L[5])};
+  };
 
   // Ray(o, d): stores origin, normalised direction and t-limit to the LDS slot.
   auto emit_ray = [&](D3 o, D3 dir, double t_limit) {
@@ -524,12 +476,9 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
             const uint32_t id = wk < n_list ? P.list[wk / P.nsamp] : 0xffffffffu;
             px = id != 0xffffffffu ? (int)(id % (uint32_t)P.W) : P.W;
             lrow = id != 0xffffffffu ? (int)(id / (uint32_t)P.W) : P.rows;
-            item = (int)wk;
+            item = wk;
           } else {
             long long tile = wk >> 6;
-#ifdef RT_EXP_REVERSE   // experiment: fetch each XCD range's tiles in reverse order
-            tile = ((g0 >> 6) + (g1 >> 6) - 1) - tile;
-#endif
             const int j = (int)(wk & 63);
             frame = P.n_frames > 1 ? (int)(tile / P.frame_tiles) : 0;
             tile -= (long long)frame * P.frame_tiles;
@@ -542,7 +491,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
             py = (P.stripe_count == 1)
                      ? P.row_begin + lrow
                      : ((lrow / P.stripe_h) * P.stripe_count + P.stripe_index) * P.stripe_h + (lrow % P.stripe_h);
-            sample = P.list ? item % P.nsamp : 0;
+            sample = P.list ? (int)(item % P.nsamp) : 0;
             start_sample();
           }
         }
@@ -652,6 +601,13 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
       };
       const D3 c3 = d3(-rd.x, -rd.y, -rd.z);
 
+      // wave-level iterations of this round; wave-uniform (SALU only), so the watchdog
+      // costs the node loop no VALU
+      uint32_t wit = 0;
+      auto trav_guard = [&]() -> bool {
+        wit = __builtin_amdgcn_readfirstlane(wit) + 1u;
+        return wit > kTravGuard;
+      };
       // tests the triangles of leaf `lref` in record order; true = any-hit ray occluded
       auto test_leaf = [&](uint32_t lref) -> bool {
           // 2-wide: iterate reference slots in order (the oracle's order); 4-wide: device
@@ -661,6 +617,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
           const uint32_t leaf0 = i;
           bool occluded = false;
           for (;;) {
+            if (trav_guard()) break;
             const uint32_t rec = (WIDTH == 2) ? P.slot2dev[i] : i;
             if (STATS) {
               c_tris++;
@@ -669,11 +626,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
               const uint32_t i0 = __shfl(i, __ffsll((long long)__ballot(1)) - 1);
               if (__ballot(i != i0) == 0) wave_tick(d_leaf_uni, d_dummy, lane);
             }
-            TriOps T;
-            if (RT_SCALAR_UNIFORM && __ballot(rec != __builtin_amdgcn_readfirstlane(rec)) == 0)
-              T = load_tri_uniform(P.tris, __builtin_amdgcn_readfirstlane(rec));
-            else
-              T = load_tri(P.tris, rec, true);
+            const TriOps T = load_tri(P.tris, rec);
             const int slot = (int)(T.meta & kSlotMask);
             // Mesh::intersect_triangle (mymesh.cpp:190-215): the same fp64 S, Da, Db, Dt as
             // the CPU (bit-identical operands and operation order).  Division-free early
@@ -724,9 +677,16 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
       uint32_t pleaf = kDone;   // 4-wide: postponed leaf
 
       while (__ballot(cur != kDone || pleaf != kDone) != 0) {
+        if (trav_guard()) {   // watchdog: abandon the round (results void, launch flagged)
+          if (lane == __ffsll((long long)__ballot(1)) - 1) atomicOr(&P.ctr[CD_GUARD], 1ull);
+          cur = kDone;
+          pleaf = kDone;
+          break;
+        }
         if (STATS) wave_tick(d_round_it, d_round_ln, lane);
         if constexpr (WIDTH == 2) {
         while (!(cur & kLeaf)) {   // internal node (kDone carries the leaf bit)
+          if (trav_guard()) break;
           if (STATS) { c_nodes++; wave_tick(d_node_it, d_node_ln, lane); wave_distinct(cur, d_node_lines, lane); }
           const float4* nq = reinterpret_cast<const float4*>(P.nodes + cur);
           const float4 bx = nq[0], by = nq[1], bz = nq[2];
@@ -757,33 +717,11 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
         }
         } else {
         while (!(cur & kLeaf)) {   // 4-wide node: test 4 boxes, visit nearest, push the rest far-first
+          if (trav_guard()) break;
           if (STATS) { c_nodes++; wave_tick(d_node_it, d_node_ln, lane); wave_distinct(cur, d_node_lines, lane); }
           float k[4];
           uint32_t v[4];
           int cnt = 0;
-#if RT_QNODE
-          // quantised node: t = q * (scale * inv) + (origin * inv - o * inv); the scale is a
-          // power of two, so scale * inv is exact
-          const float4* nq = reinterpret_cast<const float4*>(P.nodes4q + cur);
-          const float4 a0 = nq[0], a1 = nq[1];
-          const uint4 qy = *reinterpret_cast<const uint4*>(nq + 2);
-          const uint4 rf = *reinterpret_cast<const uint4*>(nq + 3);
-          const float Ax = ivx * a0.w, Ay = ivy * a1.x, Az = ivz * a1.y;
-          const float Bx = __builtin_fmaf(a0.x, ivx, -oix), By = __builtin_fmaf(a0.y, ivy, -oiy),
-                      Bz = __builtin_fmaf(a0.z, ivz, -oiz);
-          const uint32_t qlx = __float_as_uint(a1.z), qhx = __float_as_uint(a1.w);
-          const uint32_t nqx = nxo ? qhx : qlx, fqx = nxo ? qlx : qhx;
-          const uint32_t nqy = nyo != 32u ? qy.y : qy.x, fqy = nyo != 32u ? qy.x : qy.y;
-          const uint32_t nqz = nzo != 64u ? qy.w : qy.z, fqz = nzo != 64u ? qy.z : qy.w;
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const float tx0 = __builtin_fmaf((float)((nqx >> (8 * c)) & 255u), Ax, Bx);
-            const float tx1 = __builtin_fmaf((float)((fqx >> (8 * c)) & 255u), Ax, Bx);
-            const float ty0 = __builtin_fmaf((float)((nqy >> (8 * c)) & 255u), Ay, By);
-            const float ty1 = __builtin_fmaf((float)((fqy >> (8 * c)) & 255u), Ay, By);
-            const float tz0 = __builtin_fmaf((float)((nqz >> (8 * c)) & 255u), Az, Bz);
-            const float tz1 = __builtin_fmaf((float)((fqz >> (8 * c)) & 255u), Az, Bz);
-#else
           float4 nx, fx, ny, fy, nz, fz;
           uint4 rf;
           // wave-uniform: every active lane's node is in the LDS treelet -> ds_read, no TD cost
@@ -797,30 +735,12 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
             nz = *reinterpret_cast<const float4*>(lb + nzo);
             fz = *reinterpret_cast<const float4*>(lb + (nzo ^ 16u));
             rf = *reinterpret_cast<const uint4*>(lb + 96);
-          } else if (RT_SCALAR_UNIFORM && __ballot(cur != __builtin_amdgcn_readfirstlane(cur)) == 0) {
-            // one node for the whole wave: scalar loads, per-lane near/far selection
-            const cfloat4* sn = (const cfloat4*)(uintptr_t)(P.nodes4) +
-                                (size_t)__builtin_amdgcn_readfirstlane(cur) * (sizeof(GNode4) / sizeof(float4));
-            const f4v lx = sn[0], hx = sn[1], ly = sn[2], hy = sn[3], lz = sn[4], hz = sn[5];
-            const f4v r4 = sn[6];
-            const bool px_ = nxo == 0u, py_ = nyo == 32u, pz_ = nzo == 64u;
-            auto sel = [](bool c, const f4v& a, const f4v& b) {
-              return make_float4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
-            };
-            nx = sel(px_, lx, hx); fx = sel(px_, hx, lx);
-            ny = sel(py_, ly, hy); fy = sel(py_, hy, ly);
-            nz = sel(pz_, lz, hz); fz = sel(pz_, hz, lz);
-            rf = make_uint4(__float_as_uint(r4.x), __float_as_uint(r4.y), __float_as_uint(r4.z), __float_as_uint(r4.w));
           } else {
             const char* nb = reinterpret_cast<const char*>(P.nodes4) + (size_t)cur * sizeof(GNode4);
             if (STATS) {
               wave_distinct(cur, d_gn_dist, lane);
               const uint32_t c0 = __shfl(cur, __ffsll((long long)__ballot(1)) - 1);
               if (__ballot(cur != c0) == 0) wave_tick(d_gn_uni, d_dummy, lane);
-            }
-            if (RT_EXP_DUP & 1) {
-#pragma unroll
-              for (int k = 0; k < 7; ++k) exp_dup_load(reinterpret_cast<const float4*>(nb) + (k == 6 ? 6 : k));
             }
             nx = *reinterpret_cast<const float4*>(nb + nxo);
             fx = *reinterpret_cast<const float4*>(nb + (nxo ^ 16u));
@@ -835,26 +755,10 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
             const float tx0 = __builtin_fmaf(f4c(nx, c), ivx, -oix), tx1 = __builtin_fmaf(f4c(fx, c), ivx, -oix);
             const float ty0 = __builtin_fmaf(f4c(ny, c), ivy, -oiy), ty1 = __builtin_fmaf(f4c(fy, c), ivy, -oiy);
             const float tz0 = __builtin_fmaf(f4c(nz, c), ivz, -oiz), tz1 = __builtin_fmaf(f4c(fz, c), ivz, -oiz);
-#endif
             const float tn = fmaxf(fmaxf(tx0, ty0), fmaxf(tz0, lo_c));
             const float tf = fminf(fminf(tx1, ty1), fminf(tz1, hi_c));
-#if RT_EXP_DUP & 8   // perturbation: a second, unused copy of the slab arithmetic (VALU sensitivity)
-            {
-              float ivx2 = ivx, ivy2 = ivy, ivz2 = ivz;
-              asm volatile("" : "+v"(ivx2), "+v"(ivy2), "+v"(ivz2));
-              const float a0 = __builtin_fmaf(f4c(nx, c), ivx2, -oix), a1 = __builtin_fmaf(f4c(fx, c), ivx2, -oix);
-              const float b0 = __builtin_fmaf(f4c(ny, c), ivy2, -oiy), b1 = __builtin_fmaf(f4c(fy, c), ivy2, -oiy);
-              const float d0 = __builtin_fmaf(f4c(nz, c), ivz2, -oiz), d1 = __builtin_fmaf(f4c(fz, c), ivz2, -oiz);
-              const float tn2 = fmaxf(fmaxf(a0, b0), fmaxf(d0, lo_c)), tf2 = fminf(fminf(a1, b1), fminf(d1, hi_c));
-              asm volatile("" ::"v"(tn2), "v"(tf2));
-            }
-#endif
             const uint32_t r = u4c(rf, c);
-#if RT_EMPTY_BOX
             const bool h = tn <= tf;   // absent children carry the empty box [+inf, -inf]
-#else
-            const bool h = (tn <= tf) && (r != kEmpty);
-#endif
             k[c] = h ? tn : INFINITY;
             v[c] = r;
             cnt += h ? 1 : 0;
@@ -874,19 +778,17 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
             if (cnt > 1) push(v[1]);
             cur = v[0];
           }
-          if (RT_SPECULATIVE) {
-            if ((cur & kLeaf) && cur != kDone && pleaf == kDone) {   // first leaf: postpone, keep going
-              pleaf = cur;
-              cur = pop();
-            }
-            if (__ballot(pleaf == kDone && cur != kDone) == 0) break;   // every lane holds a leaf
+          if ((cur & kLeaf) && cur != kDone && pleaf == kDone) {   // first leaf: postpone, keep going
+            pleaf = cur;
+            cur = pop();
           }
+          if (__ballot(pleaf == kDone && cur != kDone) == 0) break;   // every lane holds a leaf
         }
         }
         // leaves: 2-wide -- the leaf the lane stopped at; 4-wide -- the postponed leaf, then
         // any leaf the lane stopped at after it (chained), so lanes that found leaves early
         // kept traversing instead of idling (speculative while-while, Aila & Laine 2009)
-        if constexpr (WIDTH == 2 || !RT_SPECULATIVE) {
+        if constexpr (WIDTH == 2) {
           if (cur != kDone) {
             if (test_leaf(cur)) cur = kDone;
             else cur = pop();
@@ -919,7 +821,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
     {
       const int idle_state = heads_left > 0 ? ST_FETCH : ST_DONE;
       if (state == ST_HSHADOW) {
-        if (shadow_hit) atomicOr(&lvis[wbase + (int)(htask & 63u)], 1u << ((htask >> 8) & 31u));
+        if (shadow_hit) atomicOr(&lvis[wbase + (int)(htask & 63u)], 1u << ((htask >> 8) & 31u));   // bit: light - batch start
         state = idle_state;
       } else if (state == ST_HCLOSEST) {
         ltask[threadIdx.x] = (uint32_t)best;
@@ -938,8 +840,8 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
       double mirror = 0.0;
       // lighting() for one light (mytracer.cpp:579-606): Lambert + Phong term of light j
       auto contrib_of = [&](int j, D3 hp_, D3 hn_, D3 hv_, D3 hd_, const GMat& M) {
-        const double* L6 = lds_lights + 6 * j;
-        const D3 l = normalize(sub(d3(L6[0], L6[1], L6[2]), hp_));
+        const Light6 L6 = light_of(j);
+        const D3 l = normalize(sub(L6.pos, hp_));
         const double diff = stdmax(0.0, dot(hn_, l));
         double refl = 0.0;
         if (diff > 0.0) {   // reflection(), mytracer.cpp:524-534
@@ -948,18 +850,13 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
           refl = stdmax(0.0, dot(r, hv_));
         }
         // pow(+0, y > 0) = +0 exactly: skip the fp64 pow for the (frequent) zero highlight
-#ifdef RT_EXP_NOPOW   // perturbation knob (wrong pixels): prices the fp64 pow
-        if (!(refl == 0.0 && M.shininess > 0.0)) refl = refl * M.shininess;
-#else
         if (!(refl == 0.0 && M.shininess > 0.0)) refl = pow(refl, M.shininess);
-#endif
-        return d3(L6[3] * (hd_.x * diff + M.ks[0] * refl), L6[4] * (hd_.y * diff + M.ks[1] * refl),
-                  L6[5] * (hd_.z * diff + M.ks[2] * refl));
+        return d3(L6.col.x * (hd_.x * diff + M.ks[0] * refl), L6.col.y * (hd_.y * diff + M.ks[1] * refl),
+                  L6.col.z * (hd_.z * diff + M.ks[2] * refl));
       };
       // own shadow ray for light `light`; the rest of the bounce is offered to idle lanes
       auto launch_batch = [&](D3 hp_, double mirror_) {
-        const double* L6 = lds_lights + 6 * light;
-        const D3 to_l = sub(d3(L6[0], L6[1], L6[2]), hp_);
+        const D3 to_l = sub(light_of(light).pos, hp_);
         const D3 l = normalize(to_l);
         c_shadow++;
         emit_ray(add(hp_, scl(1e-4, l)), l, sqrt(dot(to_l, to_l)));
@@ -967,8 +864,9 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
         lvis[threadIdx.x] = 0u;
         batch_end = light + 1;
         refl_h = -1;
-        want = RT_FANOUT == 0 ? 0
-               : (P.n_lights - light - 1) + ((RT_FANOUT > 1 && mirror_ > 0.0 && depth < P.max_depth) ? 1 : 0);
+        // extra lights of this batch, then the reflection ray once the batch covers every light
+        const int rest = P.n_lights - light - 1;
+        want = min(rest, kBatchExtra) + ((rest <= kBatchExtra && mirror_ > 0.0 && depth < P.max_depth) ? 1 : 0);
       };
       if (state == ST_SHADOW) {   // batch finished: lights [light, batch_end) in order
         hp = LD3(F_HP); hn = LD3(F_HN); hview = LD3(F_HVIEW);
@@ -978,7 +876,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
         const GMat& M = P.mats[mesh];
         const uint32_t vw = lvis[threadIdx.x];
         for (int j = light; j < batch_end; ++j) {
-          const bool occluded = (j == light) ? shadow_hit : (((vw >> j) & 1u) != 0u);
+          const bool occluded = (j == light) ? shadow_hit : (((vw >> (j - light)) & 1u) != 0u);
           // an occluded light adds colour * 0 * (finite term) = +-0, which leaves the sum (never -0)
           // unchanged: skip it (the term is finite for any material with finite shininess >= 0)
           if (!occluded) lacc = add(lacc, contrib_of(j, hp, hn, hview, hdiff, M));
@@ -1150,7 +1048,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
         const int got = min(want, max(0, avail - off));
         if (got > 0) {
           const D3 hp = LD3(F_HP);
-          const int n_extra_lights = P.n_lights - light - 1;
+          const int n_extra_lights = min(P.n_lights - light - 1, kBatchExtra);
           for (int t = 0; t < got; ++t) {
             const int ht = wbase + kth_set_bit(I, off + t);
             D3 o, d;
@@ -1158,13 +1056,12 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
             uint32_t tw;
             if (t < n_extra_lights) {
               const int j = light + 1 + t;
-              const double* L6 = lds_lights + 6 * j;
-              const D3 to_l = sub(d3(L6[0], L6[1], L6[2]), hp);
+              const D3 to_l = sub(light_of(j).pos, hp);
               const D3 l = normalize(to_l);
               o = add(hp, scl(1e-4, l));
               d = normalize(l);
               tl = sqrt(dot(to_l, to_l));
-              tw = (uint32_t)lane | ((uint32_t)j << 8);
+              tw = (uint32_t)lane | ((uint32_t)(t + 1) << 8);
               c_shadow++;
             } else {   // reflection ray (same formula as the owner's own emission)
               const D3 hn = LD3(F_HN), hv = LD3(F_HVIEW);
@@ -1448,16 +1345,15 @@ struct rt_scene {
   int next_ctx = 0;             // ring cursor
   int last_ctx = -1;            // context of the most recent launch
   size_t nslots = 0;
-  double* d_lights = nullptr;   // [RT_MAX_LIGHTS][6]
-  int cached_lights = -1;       // light count currently in d_lights
-  double cached_light_data[RT_MAX_LIGHTS * 6] = {};
+  double* d_lights = nullptr;   // [light_cap][6] position xyz, colour rgb
+  int light_cap = 0;            // lights d_lights can hold
+  std::vector<double> cached_light_data;   // the table currently in d_lights
   double delta = 0.0;
   double root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};
   long long bytes = 0;
   int n_cu = 0;
   int blocks_per_cu[kNumVariants] = {0, 0, 0};
   GNode4* d_nodes4 = nullptr;
-  GNode4Q* d_nodes4q = nullptr;
   int n_gnodes4 = 0;
   int n_top = 0;                // 4-wide nodes each block caches in LDS
   std::vector<GMat> mesh_mats;  // host copy: the analytic materials are appended after these
@@ -2273,48 +2169,6 @@ void build_sbvh_tree(const rt_scene_soa* s, DevTree& E, std::vector<uint32_t>& r
   tick("merge");
 }
 
-// GNode4 -> GNode4Q: per axis, origin = union low corner (fp32), scale = the smallest power
-// of two with 255 * scale >= extent; child planes rounded outward onto the grid (exact in
-// double), so the decoded box contains the fp32 box.
-GNode4Q quantise_node(const GNode4& g) {
-  GNode4Q q;
-  std::memset(&q, 0, sizeof q);
-  const float* lo[3] = {g.lox, g.loy, g.loz};
-  const float* hi[3] = {g.hix, g.hiy, g.hiz};
-  float org[3], scl[3];
-  uint32_t qlo[3] = {0, 0, 0}, qhi[3] = {0, 0, 0};
-  for (int k = 0; k < 3; ++k) {
-    float plo = INFINITY, phi = -INFINITY;
-    for (int c = 0; c < 4; ++c)
-      if (g.ref[c] != kEmpty) { plo = std::min(plo, lo[k][c]); phi = std::max(phi, hi[k][c]); }
-    if (!(plo <= phi)) { plo = 0.f; phi = 0.f; }
-    const double ext = (double)phi - (double)plo;
-    double sc = 1.0;
-    if (ext > 0.0) {
-      int e = 0;
-      std::frexp(ext / 255.0, &e);   // ext/255 <= 2^e
-      sc = std::ldexp(1.0, e);
-    }
-    org[k] = plo;
-    scl[k] = (float)sc;
-    for (int c = 0; c < 4; ++c) {
-      uint32_t a = 255u, b = 0u;   // empty interval
-      if (g.ref[c] != kEmpty) {
-        const double fl = std::floor(((double)lo[k][c] - (double)plo) / sc);
-        const double ce = std::ceil(((double)hi[k][c] - (double)plo) / sc);
-        a = (uint32_t)std::min(255.0, std::max(0.0, fl));
-        b = (uint32_t)std::min(255.0, std::max(0.0, ce));
-      }
-      qlo[k] |= a << (8 * c);
-      qhi[k] |= b << (8 * c);
-    }
-  }
-  q.ox = org[0]; q.oy = org[1]; q.oz = org[2];
-  q.sx = scl[0]; q.sy = scl[1]; q.sz = scl[2];
-  q.qlo_x = qlo[0]; q.qhi_x = qhi[0]; q.qlo_y = qlo[1]; q.qhi_y = qhi[1]; q.qlo_z = qlo[2]; q.qhi_z = qhi[2];
-  for (int c = 0; c < 4; ++c) q.ref[c] = g.ref[c];
-  return q;
-}
 
 int validate(const rt_scene_soa* s, const rt_bvh_soa* b) {
   if (!s || !b) return fail(RT_ERR_INVALID, "rt_scene_upload: null scene or bvh");
@@ -2698,11 +2552,6 @@ int rt_scene_upload_ex(const rt_scene_soa* s, const rt_bvh_soa* b, int device, c
   rc = RT_OK;
   if (rc == RT_OK) rc = upload(&sc->d_nodes, nodes, bytes);
   if (rc == RT_OK) rc = upload(&sc->d_nodes4, nodes4, bytes);
-  if (RT_QNODE && rc == RT_OK) {
-    std::vector<GNode4Q> nodes4q(nodes4.size());
-    for (size_t gi = 0; gi < nodes4.size(); ++gi) nodes4q[gi] = quantise_node(nodes4[gi]);
-    rc = upload(&sc->d_nodes4q, nodes4q, bytes);
-  }
   if (rc == RT_OK) rc = upload(&sc->d_tris, tris, bytes);
   if (rc == RT_OK) rc = upload(&sc->d_slot2dev, slot2dev, bytes);
   if (rc == RT_OK) rc = upload(&sc->d_shade, shade, bytes);
@@ -2751,6 +2600,7 @@ int rt_scene_upload_ex(const rt_scene_soa* s, const rt_bvh_soa* b, int device, c
     rt_scene_free(sc);
     return fail(RT_ERR_HIP, "hipMalloc of lights failed");
   }
+  sc->light_cap = RT_MAX_LIGHTS;
   sc->bytes += (long long)(RT_MAX_LIGHTS * 6 * sizeof(double));
   for (LaunchCtx& c : sc->ctx) {
     const size_t pb = sc->nslots * kFields * sizeof(double);
@@ -2814,7 +2664,8 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
       return fail(RT_ERR_INVALID, "rt_launch_frames: frames may differ only in camera position and direction");
   }
   if (p->camera.width <= 0 || p->camera.height <= 0) return fail(RT_ERR_INVALID, "bad image size");
-  if (p->n_lights < 0 || p->n_lights > RT_MAX_LIGHTS) return fail(RT_ERR_INVALID, "n_lights out of range");
+  if (p->n_lights < 0 || p->n_lights > (p->lights_ext ? RT_LIGHTS_LIMIT : RT_MAX_LIGHTS))
+    return fail(RT_ERR_INVALID, "n_lights out of range (more than RT_MAX_LIGHTS lights need lights_ext)");
   if (p->spp_n < 1 || p->spp_n > 64) return fail(RT_ERR_INVALID, "spp_n must be in [1, 64]");
   if (p->max_depth < 0) return fail(RT_ERR_INVALID, "max_depth must be >= 0");
   if (p->out_format != RT_OUT_RGB_F32 && p->out_format != RT_OUT_RGB_F64) return fail(RT_ERR_INVALID, "bad out_format");
@@ -2828,7 +2679,7 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
 
   KParams P;
   std::memset(&P, 0, sizeof P);
-  P.nodes = sc->d_nodes; P.nodes4 = sc->d_nodes4; P.nodes4q = sc->d_nodes4q; P.tris = sc->d_tris; P.slot2dev = sc->d_slot2dev; P.shade = sc->d_shade; P.tnorm = sc->d_tnorm;
+  P.nodes = sc->d_nodes; P.nodes4 = sc->d_nodes4; P.tris = sc->d_tris; P.slot2dev = sc->d_slot2dev; P.shade = sc->d_shade; P.tnorm = sc->d_tnorm;
   P.tu = sc->d_tu; P.tv = sc->d_tv; P.texels = sc->d_texels; P.mats = sc->d_mats;
   P.prims = sc->d_prims; P.n_prims = sc->n_prims;
   LaunchCtx& C = sc->ctx[sc->next_ctx];
@@ -2847,14 +2698,24 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   P.n_lights = p->n_lights;
   P.max_depth = p->max_depth;
   {  // lights live in device memory; re-uploaded (device-synchronising) only when they change
-    double ld[RT_MAX_LIGHTS * 6] = {};
-    for (int i = 0; i < p->n_lights; ++i)
-      for (int k = 0; k < 3; ++k) { ld[6 * i + k] = p->lights[i].position[k]; ld[6 * i + 3 + k] = p->lights[i].color[k]; }
-    if (sc->cached_lights != p->n_lights || std::memcmp(ld, sc->cached_light_data, sizeof(double) * 6 * p->n_lights) != 0) {
-      HIP_TRY(hipDeviceSynchronize());
-      HIP_TRY(hipMemcpy(sc->d_lights, ld, sizeof ld, hipMemcpyHostToDevice));
-      std::memcpy(sc->cached_light_data, ld, sizeof ld);
-      sc->cached_lights = p->n_lights;
+    std::vector<double> ld(6 * (size_t)p->n_lights);
+    for (int i = 0; i < p->n_lights; ++i) {
+      const rt_light* L = rt_params_light(p, i);
+      for (int k = 0; k < 3; ++k) { ld[6 * i + k] = L->position[k]; ld[6 * i + 3 + k] = L->color[k]; }
+    }
+    if (ld != sc->cached_light_data) {
+      HIP_TRY(hipDeviceSynchronize());   // launches in flight may still read the old table
+      if (p->n_lights > sc->light_cap) {
+        HIP_TRY(hipFree(sc->d_lights));
+        sc->d_lights = nullptr;
+        sc->bytes -= (long long)(sc->light_cap * 6 * sizeof(double));
+        sc->light_cap = 0;
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&sc->d_lights), ld.size() * sizeof(double)));
+        sc->light_cap = p->n_lights;
+        sc->bytes += (long long)(ld.size() * sizeof(double));
+      }
+      if (!ld.empty()) HIP_TRY(hipMemcpy(sc->d_lights, ld.data(), ld.size() * sizeof(double), hipMemcpyHostToDevice));
+      sc->cached_light_data = std::move(ld);
     }
   }
   P.lights = sc->d_lights;
@@ -3157,7 +3018,7 @@ void rt_scene_free(rt_scene* sc) {
   (void)hipSetDevice(sc->device);
   (void)hipDeviceSynchronize();   // launches may still be reading the scene
   void* ptrs[] = {sc->d_nodes, sc->d_nodes4, sc->d_tris, sc->d_shade, sc->d_tnorm, sc->d_tu,
-                  sc->d_tv, sc->d_texels, sc->d_mats, sc->d_lights, sc->d_slot2dev, sc->d_prims, sc->d_nodes4q};
+                  sc->d_tv, sc->d_texels, sc->d_mats, sc->d_lights, sc->d_slot2dev, sc->d_prims};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   for (LaunchCtx& c : sc->ctx) {

@@ -537,11 +537,13 @@ int rt_host_camera(const rt_host_scene* s, int width, int height, rt_camera* out
 int rt_host_render_params(const rt_host_scene* s, int width, int height, int spp_n, rt_render_params* out) {
   if (!s || !out) return host_fail("rt_host_render_params: null argument");
   const rt::HostScene& sc = s->scene;
-  if ((int)sc.lights.size() > RT_MAX_LIGHTS) return host_fail("rt_host_render_params: too many lights");
+  if ((long long)sc.lights.size() > RT_LIGHTS_LIMIT) return host_fail("rt_host_render_params: too many lights");
   std::memset(out, 0, sizeof *out);
   rt::derive_camera(sc.camera, width, height, out->camera);
   out->n_lights = (int)sc.lights.size();
-  for (int i = 0; i < out->n_lights; ++i) out->lights[i] = sc.lights[i];
+  for (int i = 0; i < std::min(out->n_lights, RT_MAX_LIGHTS); ++i) out->lights[i] = sc.lights[i];
+  // more than the inline table holds: point at the scene's own list (valid while s lives)
+  out->lights_ext = out->n_lights > RT_MAX_LIGHTS ? sc.lights.data() : nullptr;
   for (int k = 0; k < 3; ++k) { out->background[k] = sc.background[k]; out->ambience[k] = sc.ambience[k]; }
   out->max_depth = sc.max_depth;
   out->spp_n = spp_n > 0 ? spp_n : 1;

@@ -12,6 +12,7 @@ RT_ERR_INVALID = -1
 RT_ERR_HIP = -2
 RT_ERR_UNSUPPORTED = -3
 RT_MAX_LIGHTS = 16
+RT_LIGHTS_LIMIT = 1 << 20
 RT_MAX_FRAMES = 128
 RT_DRAW_FLAT = 0
 RT_DRAW_PHONG = 1
@@ -95,7 +96,25 @@ class RenderParams(C.Structure):
                 ("lights", Light * RT_MAX_LIGHTS), ("background", c_double3),
                 ("ambience", c_double3), ("spp_n", C.c_int), ("row_begin", C.c_int),
                 ("row_end", C.c_int), ("stripe_height", C.c_int), ("stripe_count", C.c_int),
-                ("stripe_index", C.c_int), ("out_format", C.c_int), ("flags", C.c_int)]
+                ("stripe_index", C.c_int), ("out_format", C.c_int), ("flags", C.c_int),
+                ("lights_ext", C.POINTER(Light))]
+
+    def set_lights(self, lights):
+        """Sets the light list; more than RT_MAX_LIGHTS go through lights_ext (the array is
+        kept alive on this object)."""
+        n = len(lights)
+        self.n_lights = n
+        if n <= RT_MAX_LIGHTS:
+            self.lights_ext = None
+            arr = self.lights
+        else:
+            arr = (Light * n)()
+            self._lights_keep = arr
+            self.lights_ext = C.cast(arr, C.POINTER(Light))
+        for i, (pos, col) in enumerate(lights):
+            for k in range(3):
+                arr[i].position[k] = pos[k]
+                arr[i].color[k] = col[k]
 
 
 class Stats(C.Structure):

@@ -776,7 +776,7 @@ static void lighting(const or_ctx* C, const rt_render_params* p, const hit_t* h,
   col[0] = 0.0; col[1] = 0.0; col[2] = 0.0;
   for (int k = 0; k < 3; ++k) col[k] += p->ambience[k] * mat->ambient[k];
   for (int li = 0; li < p->n_lights; ++li) {
-    const rt_light* L = &p->lights[li];
+    const rt_light* L = rt_params_light(p, li);
     const double diff = diffuse_term(h->p, h->n, L->position);
     double refl = reflection_term(h->p, h->n, view, L->position);
     refl = pow(refl, mat->shininess);
@@ -859,7 +859,7 @@ static void add_counts(or_counts* dst, const or_counts* src) {
 
 int or_render_pixels(or_ctx* C, const rt_render_params* p, int mode, int nthreads, const int* xy,
                      long long n_pixels, double* out, or_counts* counts) {
-  if (!C || !p || p->n_lights < 0 || p->n_lights > RT_MAX_LIGHTS) return -1;
+  if (!C || !p || p->n_lights < 0 || p->n_lights > (p->lights_ext ? RT_LIGHTS_LIMIT : RT_MAX_LIGHTS)) return -1;
   or_counts total;
   memset(&total, 0, sizeof total);
 #ifdef _OPENMP

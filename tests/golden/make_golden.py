@@ -34,8 +34,11 @@ SCENE_CASES = {
 }
 
 
-def main():
+def main(only=()):
+    """only: regenerate just these KAT scene names (the other files stay untouched)."""
     for name in kat_scenes.scenes():
+        if only and name not in only:
+            continue
         for spp in (1, 2):
             mini = kat_scenes.mini(name)
             img = np.array(mini.render(spp))
@@ -43,6 +46,8 @@ def main():
                                 counts=np.array([mini.counts["primary"], mini.counts["shadow"],
                                                  mini.counts["reflection"]]))
     for fname, (kind, kw, w, h, spp) in SCENE_CASES.items():
+        if only:
+            break
         hs = rtamd.HostScene.generate(kind, **kw)
         hs.prepare()
         orc = pyoracle.Oracle(hs.raw, hs)
@@ -58,4 +63,4 @@ def main():
 
 if __name__ == "__main__":
     with tempfile.TemporaryDirectory():
-        main()
+        main(tuple(sys.argv[1:]))

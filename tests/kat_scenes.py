@@ -35,6 +35,14 @@ def scenes():
     pt = [(0, 2, 3), (0, 3, 1), (2, 4, 5), (2, 5, 3)]
     out["phong"] = ([minirt.Mesh(pv, pt, "PHONG", FLAT_MAT)], [((0.6, 0.8, 3.0), (0.9, 0.85, 0.8))], cam,
                     (0.0, 0.0, 0.0), (0.25, 0.25, 0.25), 1)
+    # 40 lights around an occluder over a mirror: more lights than the inline table
+    # (RT_MAX_LIGHTS = 16, so they travel through lights_ext) and more than one shadow batch
+    # per bounce (1 + 31 lights), with occlusion bits on both sides of the batch boundary
+    many = [((1.8 * ((i * 37) % 19 - 9) / 9.0, 0.4 + 0.05 * (i % 7), 1.2 + 0.06 * i),
+             (0.02 + 0.001 * (i % 11), 0.025, 0.03 - 0.0005 * (i % 5))) for i in range(40)]
+    out["many_lights"] = ([minirt.Mesh(mv, [(0, 1, 2), (0, 2, 3)], "FLAT", MIRROR_MAT),
+                           minirt.Mesh(ov, ot, "FLAT", FLAT_MAT)],
+                          many, cam, (0.05, 0.1, 0.2), (0.2, 0.2, 0.2), 2)
     return out
 
 

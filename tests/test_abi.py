@@ -16,6 +16,7 @@ ROOT = Path(__file__).resolve().parents[1]
 def declared(header):
     text = (ROOT / "include" / header).read_text()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    text = re.sub(r"static inline[^{]*\{.*?\n\}", "", text, flags=re.S)   # header-only helpers
     return sorted(set(re.findall(r"\b(rt_[a-z0-9_]+)\s*\(", text)))
 
 
@@ -53,6 +54,7 @@ def test_struct_layouts_match_c(tmp_path):
         src.append(f'printf("{name} %zu\\n", sizeof({name}));')
     src.append('printf("params.out_format %zu\\n", offsetof(rt_render_params, out_format));')
     src.append('printf("soa.mat_shadowable %zu\\n", offsetof(rt_scene_soa, mat_shadowable));')
+    src.append('printf("params.lights_ext %zu\\n", offsetof(rt_render_params, lights_ext));')
     src.append("return 0;}")
     (tmp_path / "sizes.c").write_text("\n".join(src))
     subprocess.run(["gcc", "-o", str(tmp_path / "sizes"), str(tmp_path / "sizes.c")], check=True)
@@ -62,6 +64,7 @@ def test_struct_layouts_match_c(tmp_path):
         assert int(got[name]) == C.sizeof(cls), name
     assert int(got["params.out_format"]) == abi.RenderParams.out_format.offset
     assert int(got["soa.mat_shadowable"]) == abi.SceneSoA.mat_shadowable.offset
+    assert int(got["params.lights_ext"]) == abi.RenderParams.lights_ext.offset
 
 
 def test_hip_entry_points_reject_bad_arguments():

@@ -311,8 +311,19 @@ def test_cli_renders(tmp_path):
     r = subprocess.run([str(ROOT / "my-raytracer_amd/bin/rt_render"), "--scene", "cornell", "--width", "64",
                         "--height", "48", "--out", str(out)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
-    assert out.read_bytes().startswith(b"P6\n64 48\n255\n")
+    data = out.read_bytes()
+    head = b"P6\n64 48\n255\n"
+    assert data.startswith(head)
     assert "Mrays/s" in r.stdout
+    # pixels: the oracle's image through the same 8-bit quantisation (rt_write_ppm: clamp,
+    # lround(v * 255), top row first).  The CLI renders fp32, so a channel may land one level
+    # off where v * 255 sits within fp32 rounding of a .5 boundary.
+    got = np.frombuffer(data[len(head):], np.uint8).reshape(48, 64, 3).astype(int)
+    hs, _, orc = Case.get("cornell")
+    ref, _ = orc.render(hs.render_params(64, 48, 1), pyoracle.MODE_REFERENCE)
+    want = np.floor(np.clip(ref[::-1].astype(np.float32), 0, 1) * np.float32(255) + 0.5).astype(int)
+    diff = np.abs(got - want)
+    assert diff.max() <= 1 and (diff == 0).mean() >= 0.999, (diff.max(), (diff != 0).sum())
 
 
 @pytest.mark.parametrize("kind,kw,w,h", [("office", {}, 192, 108), ("cornell", {}, 80, 60)])
@@ -351,26 +362,39 @@ def test_adaptive_end_to_end_and_full_frame_only():
         dev.render_adaptive(p)
 
 
+@pytest.mark.parametrize("n_lights", [rtamd.abi.RT_MAX_LIGHTS, 17, 64])
 @pytest.mark.parametrize("kind,w,h", [("cornell", 64, 48), ("office", 96, 54)])
-def test_max_lights(kind, w, h):
-    # RT_MAX_LIGHTS lights: the LDS light table at its largest and shading in several batches
-    # (more shadow rays per bounce than a wave has idle lanes to lend).
+def test_many_lights(kind, w, h, n_lights):
+    # 16 lights: the LDS light table at its largest; 17 and 64: lights_ext, read from global
+    # memory (the reference shades any nLights, mytracer_gpu.cu:632).  Shading runs in several
+    # batches (at most 1 + 31 lights per bounce and round; more shadow rays than a wave has idle
+    # lanes to lend).
     hs, dev, orc = Case.get(kind)
     p = hs.render_params(w, h, 1)
     assert p.n_lights >= 2
-    p.n_lights = rtamd.abi.RT_MAX_LIGHTS
-    for i in range(p.n_lights):
-        a = 2.0 * np.pi * i / p.n_lights
-        src = p.lights[i % 2]
-        for k in range(3):
-            p.lights[i].position[k] = src.position[k] + (0.3 * np.cos(a) if k == 0 else 0.3 * np.sin(a) if k == 2 else 0.0)
-            p.lights[i].color[k] = 0.1 + 0.02 * (i % 5)
+    base = [(tuple(p.lights[i].position), tuple(p.lights[i].color)) for i in range(2)]
+    lights = []
+    for i in range(n_lights):
+        a = 2.0 * np.pi * i / n_lights
+        pos, _ = base[i % 2]
+        lights.append(((pos[0] + 0.3 * np.cos(a), pos[1], pos[2] + 0.3 * np.sin(a)),
+                       (0.1 + 0.02 * (i % 5),) * 3))
+    p.set_lights(lights)
+    assert (p.n_lights > rtamd.abi.RT_MAX_LIGHTS) == bool(p.lights_ext)
     ref, cnt = orc.render(p, pyoracle.MODE_REFERENCE)
     p.out_format = rtamd.RT_OUT_RGB_F64
     img, st = dev.render(p)
     assert np.abs(img - ref).max() <= TOL64
     assert counts(st) == [cnt.primary_rays, cnt.shadow_rays, cnt.reflection_rays]
-    assert st.shadow_rays > 8 * st.primary_rays
+    assert st.shadow_rays > (n_lights // 2) * st.primary_rays
+
+
+def test_too_many_inline_lights_rejected():
+    hs, dev, _ = Case.get("cornell")
+    p = hs.render_params(16, 16, 1)
+    p.n_lights = rtamd.abi.RT_MAX_LIGHTS + 1     # no lights_ext: the inline table holds 16
+    with pytest.raises(rtamd.RtError):
+        dev.render(p)
 
 
 @pytest.mark.parametrize("n,stripe_h", [(2, 16), (3, 8), (4, 1)])
