@@ -8,24 +8,31 @@ One step = one full frame: every rank renders its interleaved 16-row stripes
 (stripe = rank mod N) with one launch of the flattened HIP kernel, then rank 0
 gathers the stripes over RCCL (torch.distributed "nccl") and re-interleaves
 them into the final image.  Total work per step is fixed => "strong" scaling.
-Consecutive frames are rendered --frames at a time (default 128) by ONE launch
-of the persistent kernel (rt_launch_frames: the frames share one work queue,
-so the drain at the end of a launch is paid once per F frames); every frame
-still traces all of its rays.  --streams S > 1 additionally keeps S launches in
-flight on separate streams.  Default: 1 on one GPU (launches serial, so the HIP-event
-launch duration is the kernel's own duration, as rocprofv3 reports it); 2 on N > 1,
-so the RCCL gather of launch i (and the drain of its kernel) overlaps launch i+1.
+Consecutive frames are rendered --frames at a time (default 128, at most --steps)
+by ONE launch of the persistent kernel (rt_launch_frames: the frames share one
+work queue, so the drain at the end of a launch is paid once per F frames).  The
+F frames of a launch follow an animation path (rtamd.camera_orbit, --sweep): they
+are distinct views, and every frame traces all of its rays.  A single_frame record
+(one frame per launch, the reference's use, mytracer_gpu.cu:59-81) is timed after
+the main run.  --streams S > 1 keeps S launches in flight on separate streams
+(default 1 on one GPU: launches serial, so the HIP-event launch duration is the
+kernel's own duration, as rocprofv3 reports it; 2 on N > 1, so the RCCL gather of
+launch i overlaps launch i+1).
 
-Rays per frame are the canonical counts returned by the kernel's
-counters in an untimed launch.  Roofline: algorithmic bytes per launch =
-64*node_visits + 48*tri_tests + 64*closest_hits, from the
-instrumented kernel variant (its counters are pinned to the CPU oracle's
-replica by tests/test_gpu_parity.py), divided by the kernel duration measured
-with HIP events on the launch stream over the timed steps.
+Rays are the canonical counts returned by the kernel's counters in
+untimed launches of exactly the timed launch shapes.  Roofline:
+`traffic` = HBM bytes per launch from the committed rocprofv3 --pmc summary of
+this workload (FETCH_SIZE/WRITE_SIZE per frame x frames per launch), `achieved`
+= traffic / the HIP-event launch duration, `frac` = achieved / 8 TB/s.  The
+canonical SURVEY §8d bytes (64*node_visits + 48*tri_tests + 64*closest_hits over
+the reference tree) are reported as `work_bytes_per_frame`, and `l1_roof` prices
+the production kernel's own fetches against the CU vector-L1 data path, the
+binding resource.
 
 cpu_baseline: the CPU oracle (C restatement of the reference's CPU renderer:
-recursive unordered fp64 BVH traversal, closest-hit shadow rays, OpenMP) timed
-on a deterministic row sample of the same frame, rank 0 / N=1 only.
+recursive unordered fp64 BVH traversal, closest-hit shadow rays, OpenMP on every
+CPU this process may use) timed on whole frames of the same workload, rank 0 /
+N=1 only.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        (N>1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
@@ -66,11 +73,21 @@ def parse():
     ap.add_argument("--cpu-row-stride", type=int, default=1, help="cpu_baseline renders every k-th row")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="cpu_baseline: minimum timed CPU work")
-    ap.add_argument("--save", default="", help="rank 0: save the gathered image (.npy)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="cpu_baseline threads (default: every CPU this process may run on, see usable_cpus)")
+    ap.add_argument("--save", default="", help="rank 0: save the gathered image of the last frame (.npy)")
     ap.add_argument("--frames", type=int, default=0,
-                    help="frames per launch (rt_launch_frames, <= RT_MAX_FRAMES = 128; default 128): one persistent-kernel "
-                         "launch renders F consecutive frames from one work queue, so the per-launch drain is "
-                         "paid once per F")
+                    help="frames per launch (rt_launch_frames, <= RT_MAX_FRAMES = 128, <= --steps; default 128): "
+                         "one persistent-kernel launch renders F consecutive frames from one work queue, so the "
+                         "per-launch drain is paid once per F")
+    ap.add_argument("--sweep", type=float, default=0.12,
+                    help="animation path: frame f of a launch turns the camera by sweep*(f/(F-1) - 1/2) radians "
+                         "about the image's vertical axis (rtamd.camera_orbit), so the batched frames are distinct "
+                         "views; 0 = every frame the same camera")
+    ap.add_argument("--single-frames", type=int, default=16,
+                    help="after the timed run: this many one-frame launches, timed the same way (single_frame record)")
+    ap.add_argument("--frame-budget-gb", type=float, default=8.0,
+                    help="device memory for one stream's frame buffers; caps frames per launch at large sizes")
     ap.add_argument("--streams", type=int, default=0,
                     help="launches in flight on separate streams (1 = launches strictly serial; default 1 on "
                          "one GPU, 2 on N > 1 so the RCCL gather of one launch overlaps the next launch)")
@@ -84,6 +101,13 @@ def parse():
                     help="each frame = primary pass + adaptive supersampling pass (subp 4, threshold 0.02, "
                          "mytracer_gpu.cu:83-109); N > 1: stripe-edge halo rows exchanged by one all_gather per frame")
     return ap.parse_args()
+
+
+def workload_key(a, n):
+    """Identity of the profiled workload: the PMC summary of a run applies to runs with the same key."""
+    return {"scene": a.scene, "tris": a.tris, "width": a.width, "height": a.height, "spp": a.spp, "tree": a.tree,
+            "sweep": a.sweep if not a.adaptive else 0.0, "adaptive": bool(a.adaptive),
+            "analytic": bool(a.analytic or a.scene == "spheres"), "n_gpus": n}
 
 
 def main():
@@ -117,18 +141,24 @@ def main():
     params.stripe_count = n
     params.stripe_index = rank
     W = a.width
+    rows_max = shard_max_rows(a.height, STRIPE_H, n)
     # librt_hip keeps 8 launch contexts per scene; the halo exchange of --adaptive is single-stream
     S = 1 if a.adaptive else max(1, min(a.streams or (1 if n == 1 else 2), 8))
-    F = 1 if a.adaptive else max(1, min(a.frames or 128, rtamd.abi.RT_MAX_FRAMES))
+    frame_bytes = rows_max * W * 3 * 4
+    F = 1 if a.adaptive else max(1, min(a.frames or 128, rtamd.abi.RT_MAX_FRAMES, a.steps,
+                                        int(a.frame_budget_gb * 1e9 // frame_bytes)))
+    # the animation path: frame f of every launch (the batched frames are distinct views)
+    if F > 1 and a.sweep != 0.0:
+        cams = [rtamd.camera_orbit(params, a.sweep * (f / (F - 1) - 0.5)) for f in range(F)]
+    else:
+        cams = [params] * F
     # per stream: the F frames of one launch, contiguous, so one collective gathers them
-    fbufs = [torch.zeros((F, shard_max_rows(a.height, STRIPE_H, n), W, 3), dtype=torch.float32, device="cuda")
-             for _ in range(S)]
+    fbufs = [torch.zeros((F, rows_max, W, 3), dtype=torch.float32, device="cuda") for _ in range(S)]
     bufs = [fb[f] for fb in fbufs for f in range(F)]
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(S - 1)]
-    buf = bufs[0]
     stream = streams[0].cuda_stream
     rows_local = rtamd.rows_in_shard(params)
-    prims = [torch.zeros((shard_max_rows(a.height, STRIPE_H, n), W, 3), dtype=torch.float64, device="cuda")
+    prims = [torch.zeros((rows_max, W, 3), dtype=torch.float64, device="cuda")
              for _ in range(S)] if a.adaptive else []
     # N > 1: the neighbour test of a stripe's edge rows needs the rows the neighbouring ranks
     # rendered -- ONE all_gather of every rank's stripe-edge rows per frame (rtamd.shard.HaloExchange)
@@ -143,32 +173,40 @@ def main():
         return gpu.launch_adaptive_shard(params, prim.data_ptr(), halo.data_ptr(), out.data_ptr(), 4, 0.02,
                                          stats=stats, stream=stream_)
 
-    # ---- counters: canonical rays + algorithmic bytes (untimed launches) ----
-    if F > 1:   # same launch shape as the timed ones (identical frames: counts / F are exact)
-        st = gpu.launch_frames(params, [b.data_ptr() for b in bufs[:F]], stats=True, stream=stream)
-        for f in ("primary_rays", "shadow_rays", "reflection_rays", "node_visits", "tri_tests", "closest_hits",
-                  "pixels"):
-            setattr(st, f, getattr(st, f) // F)
-    else:
-        st = gpu.launch(params, buf.data_ptr(), stats=True, stream=stream)
-    params.flags = rtamd.RT_FLAG_TRAVERSAL_STATS
-    tst = gpu.launch(params, buf.data_ptr(), stats=True, stream=stream)
-    params.flags = rtamd.RT_FLAG_WIDE_STATS   # the production kernel's own node / triangle fetches
-    wst = gpu.launch(params, buf.data_ptr(), stats=True, stream=stream)
-    params.flags = 0
-    rays_local = st.primary_rays + st.shadow_rays + st.reflection_rays
+    # ---- counters (untimed launches of exactly the timed launch shapes) ----
+    # rays of one launch of nf frames (frames cams[:nf]); the timed run is full launches of F frames
+    # plus one of steps % F frames
+    def launch_counts(nf, flags=0):
+        ps = [rtamd.abi.RenderParams.from_buffer_copy(c) for c in cams[:nf]]
+        for q in ps:
+            q.flags = flags
+        if nf == 1:
+            return gpu.launch(ps[0], bufs[0].data_ptr(), stats=True, stream=stream)
+        return gpu.launch_frames(ps, [b.data_ptr() for b in bufs[:nf]], stats=True, stream=stream)
+
+    def rays_of(st):
+        return st.primary_rays + st.shadow_rays + st.reflection_rays
+
+    n_full, rem = divmod(a.steps, F)
+    st = launch_counts(F)
+    rays_timed_local = n_full * rays_of(st) + (rays_of(launch_counts(rem)) if rem else 0)
+    st1 = launch_counts(1)                               # frame 0 alone: the single-frame record
+    rays_frame0_local = rays_of(st1)
+    tst = launch_counts(F, rtamd.RT_FLAG_TRAVERSAL_STATS)   # canonical 2-wide walk of the reference tree
+    wst = launch_counts(F, rtamd.RT_FLAG_WIDE_STATS)        # the production kernel's own fetches
     adaptive_info = None
     if a.adaptive:   # untimed: rays of the adaptive pass (selection depends on the primary image)
         p64 = rtamd.abi.RenderParams.from_buffer_copy(params)
         p64.out_format = rtamd.RT_OUT_RGB_F64
         gpu.launch(p64, prims[0].data_ptr(), stats=True, stream=stream)
-        ast, nsel = adaptive_pass(prims[0], buf, True, stream)
-        rays_local += ast.primary_rays + ast.shadow_rays + ast.reflection_rays
-        adaptive_info = {("pixels_supersampled" if n == 1 else "pixels_supersampled_rank0"): nsel, "subp": 4, "threshold": 0.02,
-                         "rays": ast.primary_rays + ast.shadow_rays + ast.reflection_rays}
-    alg_bytes_local = 64 * tst.node_visits + 48 * tst.tri_tests + 64 * tst.closest_hits
-    # bytes the production kernel requests from L1: 128-B GNode4, 80-B GTri, 96-B normal record per hit
-    fetch_bytes_local = 128 * wst.node_visits + 80 * wst.tri_tests + 96 * wst.closest_hits
+        ast, nsel = adaptive_pass(prims[0], bufs[0], True, stream)
+        rays_timed_local += a.steps * rays_of(ast)
+        rays_frame0_local += rays_of(ast)
+        adaptive_info = {("pixels_supersampled" if n == 1 else "pixels_supersampled_rank0"): nsel, "subp": 4,
+                         "threshold": 0.02, "rays": rays_of(ast)}
+    # per frame, averaged over the F frames of a launch
+    work_bytes_frame = (64 * tst.node_visits + 48 * tst.tri_tests + 64 * tst.closest_hits) / F
+    fetch_bytes_frame = (128 * wst.node_visits + 80 * wst.tri_tests + 96 * wst.closest_hits) / F
 
     gathers = [StripeGather(a.height, W, STRIPE_H, n, rank, device="cuda", frames=F, host_staged=host_staged)
                for _ in range(S)]
@@ -177,10 +215,10 @@ def main():
     starts, ends, launch_frames = [], [], []
 
     def launch(li, nf, timed):
-        """Launch li renders nf frames (steps); each frame is then gathered to rank 0."""
+        """Launch li renders nf frames (steps); their stripes are then gathered to rank 0."""
         nonlocal image
         s = streams[li % S]
-        bs = bufs[(li % S) * F:(li % S) * F + nf]
+        bs = [fbufs[li % S][f] for f in range(nf)]
         with torch.cuda.stream(s):
             if timed:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -189,55 +227,101 @@ def main():
                 gpu.launch(p64, prims[li % S].data_ptr(), stats=False, stream=s.cuda_stream)
                 adaptive_pass(prims[li % S], bs[0], False, s.cuda_stream)
             elif nf == 1:
-                gpu.launch(params, bs[0].data_ptr(), stats=False, stream=s.cuda_stream)
+                gpu.launch(cams[0], bs[0].data_ptr(), stats=False, stream=s.cuda_stream)
             else:
-                gpu.launch_frames(params, [b.data_ptr() for b in bs], stats=False, stream=s.cuda_stream)
+                gpu.launch_frames(cams[:nf], [b.data_ptr() for b in bs], stats=False, stream=s.cuda_stream)
             if timed:
                 e1.record(s)
                 starts.append(e0)
                 ends.append(e1)
                 launch_frames.append(nf)
-            image = gathers[li % S](fbufs[li % S])   # N>1: ONE RCCL gather of the F frames' stripes + re-interleave
+            # N>1: ONE RCCL gather of the nf frames' stripes + re-interleave
+            image = gathers[li % S](fbufs[li % S][:nf])
 
-    def run(steps, timed):
+    def run(steps, timed, per_launch=F):
         li, done = 0, 0
         while done < steps:
-            nf = min(F, steps - done)
+            nf = min(per_launch, steps - done)
             launch(li, nf, timed)
             li += 1
             done += nf
 
+    def timed_region(fn):
+        torch.cuda.synchronize()
+        if n > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fn()
+        if n > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        tmax = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
+        if n > 1:
+            dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        return float(tmax[0])
+
     run(a.warmup, False)
-    torch.cuda.synchronize()
-    if n > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run(a.steps, True)
-    if n > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    elapsed = timed_region(lambda: run(a.steps, True))
     kernel_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
     kernel_ms_avg = float(np.mean(kernel_ms))
     frames_per_launch = float(np.mean(launch_frames))
+    last_image = image
 
-    tot = torch.tensor([rays_local, alg_bytes_local], dtype=torch.float64, device="cuda")
-    tmax = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    # single-frame record: the reference's use, one frame per launch (mytracer_gpu.cu:59-81)
+    single = None
+    if a.single_frames > 0 and not a.adaptive:
+        starts.clear(); ends.clear(); launch_frames.clear()
+        single_elapsed = timed_region(lambda: run(a.single_frames, True, per_launch=1))
+        single = {"frames": a.single_frames, "rays_per_frame": None,
+                  "ms_per_frame": round(single_elapsed / a.single_frames * 1e3, 4),
+                  "kernel_ms_avg": round(float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)])), 4)}
+
+    tot = torch.tensor([rays_timed_local, rays_frame0_local, work_bytes_frame], dtype=torch.float64, device="cuda")
     if n > 1:
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-    rays_total = float(tot[0])
-    elapsed = float(tmax[0])
+    rays_total, rays_frame0 = float(tot[0]), float(tot[1])
 
     if rank == 0:
-        traffic = pmc_traffic(a, n, F)
         if a.save:
-            np.save(a.save, (image[0] if image.dim() == 4 else image).float().cpu().numpy())
+            img = last_image[-1] if last_image.dim() == 4 else last_image
+            np.save(a.save, img.float().cpu().numpy())
         ms_per_step = elapsed / a.steps * 1e3
-        mrays = rays_total * a.steps / elapsed / 1e6
-        achieved = alg_bytes_local * frames_per_launch / (kernel_ms_avg * 1e-3) / 1e9
-        achieved_interval = alg_bytes_local / (elapsed / a.steps) / 1e9
+        mrays = rays_total / elapsed / 1e6
+        if single is not None:
+            single["rays_per_frame"] = int(rays_frame0)
+            single["value"] = round(rays_frame0 / (single["ms_per_frame"] * 1e-3) / 1e6, 2)
+            single["unit"] = "Mrays/s"
+        pmc = pmc_per_frame(workload_key(a, n))
+        kernel_s = kernel_ms_avg * 1e-3
+        roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": None,
+                "traffic": None}
+        if pmc is not None:
+            traffic = (pmc["read"] + pmc["write"]) * frames_per_launch
+            roof["traffic"] = int(traffic)
+            roof["achieved"] = round(traffic / kernel_s / 1e9, 1)
+            roof["frac"] = round(traffic / kernel_s / 1e9 / HBM_PEAK_GBPS, 4)
+            roof["traffic_detail"] = {"read_per_frame": int(pmc["read"]), "write_per_frame": int(pmc["write"]),
+                                      "source": pmc["source"]}
+        roof.update({
+            "kernel_ms_avg": round(kernel_ms_avg, 4),
+            "frames_per_launch": frames_per_launch,
+            "note": "achieved = HBM bytes per launch (rocprofv3 FETCH_SIZE/WRITE_SIZE of this workload, per frame, "
+                    "x frames per launch; traffic) / mean launch duration (HIP events on the launch stream); "
+                    "frac = achieved / 8 TB/s.  The kernel is not HBM-bound: the scene is cache-resident and the "
+                    "binding resource is the CU's vector-L1 data path (l1_roof; DESIGN.md §5)",
+            # SURVEY §8d canonical work: 64 B per 2-wide node + 48 B per triangle test + 64 B per hit over
+            # the reference median tree -- a measure of work, served from L1/L2, not HBM bytes
+            "work_bytes_per_frame": int(work_bytes_frame),
+            "work_rate_GBps": round(work_bytes_frame * frames_per_launch / kernel_s / 1e9, 1),
+            "l1_roof": {"peak": round(L1_PEAK_GBPS, 1), "unit": "GB/s",
+                        "fetch_bytes_per_frame": int(fetch_bytes_frame),
+                        "achieved": round(fetch_bytes_frame * frames_per_launch / kernel_s / 1e9, 1),
+                        "frac": round(fetch_bytes_frame * frames_per_launch / kernel_s / 1e9 / L1_PEAK_GBPS, 4),
+                        "td_busy_frac": pmc.get("td_busy_frac") if pmc else None,
+                        "def": "128*wide_node_visits + 80*tri_tests + 96*closest_hits (production kernel) / "
+                               "(64 B/clk x 256 CUs x 2.4 GHz)"},
+        })
         out = {
             "metric": "Mrays/sec (primary+shadow+reflect), Office 1920x1080 1spp",
             "value": round(mrays, 2),
@@ -255,52 +339,30 @@ def main():
             "config": {
                 "workload": f"{a.scene}_proxy {a.width}x{a.height} spp={a.spp * a.spp} depth={params.max_depth} "
                             f"lights={params.n_lights}",
+                "workload_key": workload_key(a, n),
                 "triangles": host.triangle_count,
                 "bvh": f"host: reference median split, depth {host.bvh_depth}; device: "
                        + {"sah": "binned-SAH hierarchy, 4-wide", "sbvh": "binned SAH with spatial splits, 4-wide",
                           "reference": "reference tree refined, 4-wide"}[a.tree],
-                "rays_per_frame": int(rays_total),
-                "rays_breakdown_rank0": {"primary": st.primary_rays, "shadow": st.shadow_rays,
-                                         "reflection": st.reflection_rays},
+                "rays_per_frame": int(rays_total / a.steps),
+                "rays_breakdown_rank0_launch": {"primary": st.primary_rays, "shadow": st.shadow_rays,
+                                                "reflection": st.reflection_rays, "frames": F},
                 "parallelism": f"row-stripes x{n} (16-row interleave) + RCCL gather" if n > 1 else "single GPU",
-                "frames_per_launch": F,
+                "frames_per_launch": frames_per_launch,
+                "animation": (f"camera orbit, {a.sweep} rad over each launch's {F} frames (distinct views)"
+                              if F > 1 and a.sweep != 0.0 else "none (identical frames)"),
                 "launches_in_flight": S,
                 "adaptive_pass": adaptive_info,
                 "analytic_prims": bool(gpu.analytic),
                 "host_bvh_build_s": round(build_s, 4),
+                # frames the production kernel rendered in this process (counting launches, warm-up,
+                # timed run, single-frame run): the divisor tools/pmc_summary.py uses for per-frame bytes
+                "production_frames_rendered": (F + rem + 1 + a.warmup + a.steps + (a.single_frames if single else 0)
+                                               if not a.adaptive else None),
                 "device_scene_MB": round(gpu.device_bytes / 1e6, 1),
             },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                "traffic": traffic["bytes_per_launch"] if traffic else None,
-                "traffic_detail": traffic,
-                "kernel_ms_avg": round(kernel_ms_avg, 4),
-                "achieved_per_frame_interval": round(achieved_interval, 1),
-                "note": "achieved = alg bytes per launch (frames_per_launch frames) / mean launch duration "
-                        "(HIP events on the launch stream); achieved_per_frame_interval = alg bytes per frame / "
-                        "(elapsed / steps)",
-                "alg_bytes_per_frame": int(alg_bytes_local),
-                "alg_bytes_per_launch": int(alg_bytes_local * frames_per_launch),
-                "alg_bytes_def": "64*node_visits + 48*tri_tests + 64*closest_hits (rank-0 frame, canonical 2-wide "
-                                 "traversal of the reference tree)",
-                # The scene (nodes + triangles, a few MB) stays cache-resident: the canonical
-                # stream is served by L1 (98 % hits) and L2, so frac vs HBM exceeds 1 (SURVEY §8d
-                # caveat).  The binding roof is the CU's L1 data path; it is priced with the
-                # bytes the production kernel actually fetches.
-                "l1_roof": {"peak": round(L1_PEAK_GBPS, 1), "unit": "GB/s",
-                            "fetch_bytes_per_launch": int(fetch_bytes_local * frames_per_launch),
-                            "achieved": round(fetch_bytes_local * frames_per_launch / (kernel_ms_avg * 1e-3) / 1e9, 1),
-                            "frac": round(fetch_bytes_local * frames_per_launch / (kernel_ms_avg * 1e-3) / 1e9
-                                          / L1_PEAK_GBPS, 4),
-                            "achieved_per_frame_interval": round(fetch_bytes_local / (elapsed / a.steps) / 1e9, 1),
-                            "frac_per_frame_interval": round(fetch_bytes_local / (elapsed / a.steps) / 1e9
-                                                             / L1_PEAK_GBPS, 4),
-                            "def": "128*wide_node_visits + 80*tri_tests + 96*closest_hits (production kernel)"},
-            },
+            "single_frame": single,
+            "roofline": roof,
             "cpu_baseline": None,
         }
         if n == 1 and not a.no_cpu_baseline:
@@ -311,26 +373,37 @@ def main():
         dist.destroy_process_group()
 
 
-def pmc_traffic(a, n, F):
-    """HBM bytes per launch from the committed rocprofv3 --pmc summary of this exact launch
-    shape (profiles/r*/pmc_office1080.json: FETCH_SIZE x 2 (gfx950) + WRITE_SIZE, in bytes,
-    production kernel dispatches), or None when this run's shape was not profiled."""
-    default = (a.scene == "office" and a.width == 1920 and a.height == 1080 and a.spp == 1 and n == 1
-               and not a.adaptive and a.tree == "sbvh")
-    if not default:
-        return None
-    found = sorted(ROOT.glob("profiles/r*/pmc_office1080.json"))
-    if not found:
-        return None
-    d = json.loads(found[-1].read_text())
-    if d.get("_frames_per_launch") != F:
-        return None
-    der = d.get("_derived", {})
-    if "hbm_read_bytes_corrected" not in der or "hbm_write_bytes" not in der:
-        return None
-    return {"bytes_per_launch": int(der["hbm_read_bytes_corrected"] + der["hbm_write_bytes"]),
-            "read": int(der["hbm_read_bytes_corrected"]), "write": int(der["hbm_write_bytes"]),
-            "source": str(found[-1].relative_to(ROOT))}
+def pmc_per_frame(key):
+    """HBM bytes per frame of this workload from the newest committed rocprofv3 --pmc summary
+    (profiles/r*/pmc_*.json, tools/pmc_summary.py: production-kernel FETCH_SIZE / WRITE_SIZE summed
+    over the profiled run's dispatches, divided by the frames they rendered, with the access-width
+    corrections of profiles/r*/hbm_calib.json), or None when this workload was not profiled."""
+    best = None
+    for path in sorted(ROOT.glob("profiles/r*/pmc_*.json")):
+        try:
+            d = json.loads(path.read_text())
+        except (OSError, ValueError):
+            continue
+        if d.get("_workload") != key:
+            continue
+        pf = d.get("_per_frame", {})
+        if "hbm_read_bytes" in pf and "hbm_write_bytes" in pf:
+            best = {"read": pf["hbm_read_bytes"], "write": pf["hbm_write_bytes"],
+                    "td_busy_frac": d.get("_derived", {}).get("td_busy_frac"),
+                    "source": str(path.relative_to(ROOT))}
+    return best
+
+
+def usable_cpus():
+    """CPUs this process may actually use: its affinity mask, capped by a cgroup CPU quota."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
 
 
 def cpu_baseline(host, params, a):
@@ -339,8 +412,9 @@ def cpu_baseline(host, params, a):
     sys.path.insert(0, str(ROOT / "oracle"))
     import pyoracle
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    threads = max(1, min(threads, 16))
+    # every CPU this process may use (the reference CPU path is OpenMP over all host cores,
+    # README.md:10); on the GPU box that is the job's share of the node, not the node's nproc
+    threads = a.cpu_threads or usable_cpus()
     orc = pyoracle.Oracle(host.raw, host)
     ys = np.arange(0, a.height, a.cpu_row_stride)
     xs = np.arange(a.width)
@@ -373,6 +447,8 @@ def cpu_baseline(host, params, a):
                   f"closest-hit shadows, OpenMP over pixels)",
         "cpu_model": cpu_model,
         "nproc": os.cpu_count(),
+        "usable_cpus": usable_cpus(),
+        "affinity_cpus": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None,
         "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
     }
 

@@ -339,6 +339,26 @@ def shard_rows(height, stripe_height, stripe_count, stripe_index):
     return y[(y // stripe_height) % stripe_count == stripe_index]
 
 
+def camera_orbit(params, angle):
+    """Copy of params whose camera is turned rigidly by `angle` radians about the image's
+    vertical axis (y_dir) through the point the image centre looks at (lower_left +
+    W/2 x_dir + H/2 y_dir): eye, lower_left, x_dir and y_dir rotate together, so every frame
+    is a valid pinhole camera of the same scene.  Frames of an animation path for
+    rt_launch_frames, which lets frames differ only in these four vectors."""
+    q = abi.RenderParams.from_buffer_copy(params)
+    cam = q.camera
+    eye, ll = np.array(cam.eye[:]), np.array(cam.lower_left[:])
+    xd, yd = np.array(cam.x_dir[:]), np.array(cam.y_dir[:])
+    c = ll + 0.5 * cam.width * xd + 0.5 * cam.height * yd
+    k = yd / np.linalg.norm(yd)
+    kx = np.array([[0.0, -k[2], k[1]], [k[2], 0.0, -k[0]], [-k[1], k[0], 0.0]])
+    R = np.eye(3) + np.sin(angle) * kx + (1.0 - np.cos(angle)) * (kx @ kx)   # Rodrigues
+    for name, v in (("eye", c + R @ (eye - c)), ("lower_left", c + R @ (ll - c)), ("x_dir", R @ xd),
+                    ("y_dir", R @ yd)):
+        getattr(cam, name)[:] = [float(x) for x in v]
+    return q
+
+
 def write_ppm(path, img):
     img = np.ascontiguousarray(img, dtype=np.float32)
     h, w, _ = img.shape

@@ -44,17 +44,26 @@ class StripeGather:
         self.image = torch.empty(lead + (height, width, channels), dtype=dtype, device=device) if rank == 0 else None
 
     def __call__(self, buf):
+        """buf: this rank's packed stripes; with frames == F it may hold the first nf <= F
+        frames only ([nf, max_rows, W, C]): just those are sent, and the first nf frames of
+        the returned image are valid."""
         d = self.row_dim
         if self.n == 1:
             return buf.narrow(d, 0, self.ids[0].numel())
-        if self.rank == 0 and buf.shape != self.gather_list[0].shape:
-            raise ValueError("buffer shape does not match the gather")
-        dist.gather(buf.cpu() if self.host_staged else buf, self.gather_list, dst=0)
+        glist, image = self.gather_list, self.image
+        if self.rank == 0:
+            if d == 1 and buf.shape[0] < glist[0].shape[0]:
+                nf = buf.shape[0]
+                glist = [g[:nf] for g in glist]
+                image = image[:nf]
+            if buf.shape != glist[0].shape:
+                raise ValueError("buffer shape does not match the gather")
+        dist.gather(buf.cpu() if self.host_staged else buf, glist, dst=0)
         if self.rank == 0:
             for r in range(self.n):
-                part = self.gather_list[r].narrow(d, 0, self.ids[r].numel()).to(self.image.device)
-                self.image.index_copy_(d, self.ids[r], part)
-        return self.image
+                part = glist[r].narrow(d, 0, self.ids[r].numel()).to(image.device)
+                image.index_copy_(d, self.ids[r], part)
+        return image
 
 
 def segments(rows):
