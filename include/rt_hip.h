@@ -171,6 +171,13 @@ typedef struct rt_upload_options {
 int rt_scene_upload_ex(const rt_scene_soa* soa, const rt_bvh_soa* bvh, int device, const rt_upload_options* opt,
                        rt_scene** out);
 
+/* Uploads one scene to several devices: the device layout (hierarchy, records) is built
+ * once on the host and copied to devices[0..n_devices), one host thread per device.
+ * outs[g] receives the scene on devices[g]; on failure every outs[g] is NULL.  The
+ * multi-GPU driver (rt_multi.h) uses it. */
+int rt_scene_upload_multi(const rt_scene_soa* soa, const rt_bvh_soa* bvh, const int* devices, int n_devices,
+                          const rt_upload_options* opt, rt_scene** outs);
+
 /* Device bytes held by the scene (nodes, triangles, shading data). */
 long long rt_scene_device_bytes(const rt_scene* scene);
 

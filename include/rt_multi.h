@@ -1,0 +1,68 @@
+/*
+ * rt_multi.h — single-process multi-GPU render of one frame on one node (librt_multi.so).
+ *
+ * image rows shard embarrassingly over the GPUs of a node (pixels are
+ * independent, mytracer_gpu.cu:132-159).  GPU g of n renders the interleaved row stripes
+ * (y / stripe_height) % n == g, packed in increasing y (rt_render_params rules, the same
+ * kernel launch as rt_launch_compute_image); then ONE ncclGather (RCCL over xGMI) of the
+ * equal-size, padded stripe buffers to devices[0] and a re-interleave kernel there
+ * assemble the frame.  The scene and its device hierarchy are built once on the host and
+ * copied to every GPU (rt_scene_upload_multi).
+ *
+ * The reference renders on device 0 only (launch_compute_image_device,
+ * mytracer_gpu.cu:32-113); this is the entry its C++ host side
+ * (Raytracer::compute_image_cuda, mytracer.cpp:123-159) would call to use a whole node.
+ * One host thread drives every GPU: launches are asynchronous and the collective is one
+ * ncclGroupStart/End over the per-device communicators (ncclCommInitAll).
+ */
+#ifndef RT_MULTI_H
+#define RT_MULTI_H
+
+#include "rt_hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct rt_multi rt_multi;   /* opaque: scenes, communicators, streams, stripe buffers */
+
+/* Uploads the scene to devices[0..n_devices) and creates one RCCL communicator per device.
+ * n_devices >= 1; device ids must be distinct (RCCL allows one rank per GPU). */
+int rt_multi_create(const rt_scene_soa* soa, const rt_bvh_soa* bvh, const int* devices, int n_devices,
+                    const rt_upload_options* opt, rt_multi** out);
+
+/* Number of GPUs of the driver. */
+int rt_multi_device_count(const rt_multi* m);
+
+/* Renders one whole frame (p->row_begin / row_end / stripe_* are ignored: every row is
+ * rendered, sharded as above with the given stripe_height >= 1) into d_out, a DEVICE
+ * buffer on devices[0] holding height x width x 3 values of p->out_format, row-major,
+ * row 0 first (the layout of rt_launch_compute_image).  Synchronous.  stats (optional):
+ * ray counters summed over the GPUs; ms (optional): wall time from the first launch to
+ * the assembled frame (render + gather + re-interleave). */
+int rt_multi_render(rt_multi* m, const rt_render_params* p, int stripe_height, void* d_out, rt_stats* stats,
+                    double* ms);
+
+/* rt_multi_render into a HOST buffer (the frame is copied from devices[0] after ms is taken). */
+int rt_multi_render_to_host(rt_multi* m, const rt_render_params* p, int stripe_height, void* host_out,
+                            rt_stats* stats, double* ms);
+
+/* Rows of the largest shard: the padded stripe-buffer height every GPU sends. */
+int rt_multi_max_rows(int height, int stripe_height, int n);
+
+/* Host restatement of the frame assembly (no GPU): gathered holds n shard buffers of
+ * rt_multi_max_rows(height, stripe_height, n) x width x channels elements of elem_bytes
+ * each, shard g packed as GPU g renders it; out receives the height x width x channels
+ * frame.  Same index map as the device kernel. */
+int rt_multi_interleave_host(const void* gathered, void* out, int height, int width, int channels, int elem_bytes,
+                             int stripe_height, int n);
+
+void rt_multi_free(rt_multi* m);
+
+/* Thread-local message of the last failing rt_multi_* call. */
+const char* rt_multi_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_MULTI_H */

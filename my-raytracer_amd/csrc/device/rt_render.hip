@@ -107,6 +107,18 @@ __device__ __forceinline__ double buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t voff
 __device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, double x) {
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, x), r, voff, soff, 0);
 }
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+struct D2 {
+  double a, b;
+};
+__device__ __forceinline__ D2 buf_ld2(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+  return D2{__builtin_bit_cast(double, u32x2_t{v.x, v.y}), __builtin_bit_cast(double, u32x2_t{v.z, v.w})};
+}
+__device__ __forceinline__ void buf_st2(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, double a, double b) {
+  const u32x2_t x = __builtin_bit_cast(u32x2_t, a), y = __builtin_bit_cast(u32x2_t, b);
+  __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{x.x, x.y, y.x, y.y}, r, voff, soff, 0);
+}
 
 
 // Lane of the k-th (0-based) set bit of m (k < popcount(m)).
@@ -157,7 +169,7 @@ struct KParams {
   const unsigned char* texels;
   const GMat* mats;
   unsigned long long* ctr;
-  double* pstate;       // [kFields][nslots] path state
+  double* pstate;       // path state, [nslots / 64][kSlots][64] x 16 B
   uint32_t* spill;      // [stack_words][nslots] traversal-stack entries below the LDS ring
   unsigned long long* wavelog;  // STATS: per wave {start, last refill, end, pixels} (s_memrealtime)
   const double* lights; // [n_lights][6] position xyz, colour rgb
@@ -307,11 +319,20 @@ __device__ __forceinline__ TriOps load_tri(const GTri* tris, uint32_t i) {
   return T;
 }
 
-// Path-state fields kept in global memory, one 224-B record per lane of the
-// persistent grid.  They are touched only when a ray completes.
+// Path state kept in global memory between a lane's rays, in 16-B slots (two fp64 each),
+// wave-interleaved [wave][slot][64 lanes][2]: one slot access of a wave is one b128 buffer
+// instruction over 1 KB of contiguous lines.  Only what cannot be recomputed is kept:
+//   hit point / normal / view vector of the bounce being shaded (HP, HN, HV: 9 fp64, the
+//     record of every shadowable hit -- 4 b128 + 1 b64 stores, the same loads back);
+//   the textured diffuse colour (HD; untextured hits re-read the material's kd);
+//   the light sum across shadow batches (LACC; a bounce whose lights fit one batch
+//     restarts from the recomputed ambient term);
+//   the sample's colour and weight across mirror bounces (SCOL, W) and the pixel's sum
+//     across samples (PCOL).
+// The mirror coefficient comes from the material (the lane keeps the mesh id).
 enum : int {
-  F_PCOL = 0, F_SCOL = 3, F_W = 6, F_HP = 7, F_HN = 10, F_HVIEW = 13, F_HDIFF = 16,
-  F_LACC = 19, F_MIRROR = 22, kFields = 23
+  S_HP01 = 0, S_HP2_HN0, S_HN12, S_HV01, S_HV2, S_SCOL01, S_SCOL2_W, S_PCOL01, S_PCOL2, S_HD01, S_HD2,
+  S_LACC01, S_LACC2, kSlots
 };
 
 // LDS ray slots ([field][thread], conflict-free): the only hand-over between
@@ -373,16 +394,32 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
 
   const int lane = threadIdx.x & 63;
   const unsigned long long lane_below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  // path state, wave-interleaved [wave][field][64 lanes]: one field of a wave is 512
-  // contiguous bytes (4 lines per access instead of 64 with a per-lane record).
-  // Buffer ops: lane offset in one VGPR, field offset f*512 as an SGPR constant.
+  // path state, wave-interleaved [wave][slot][64 lanes] x 16 B (see kSlots): buffer ops
+  // with the lane offset in one VGPR and the slot offset s*1024 as an SGPR constant.
   const __amdgpu_buffer_rsrc_t prs =
-      __builtin_amdgcn_make_buffer_rsrc(P.pstate, 0, (int)(P.nslots * kFields * sizeof(double)), kBufWord3);
-  const uint32_t pvo = ((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * (uint32_t)kFields * 64u + (uint32_t)lane) * 8u;
-  auto LD = [&](int f) { return buf_ld(prs, pvo, (uint32_t)f * 512u); };
-  auto ST = [&](int f, double v) { buf_st(prs, pvo, (uint32_t)f * 512u, v); };
-  auto LD3 = [&](int f) { return d3(LD(f), LD(f + 1), LD(f + 2)); };
-  auto ST3 = [&](int f, D3 v) { ST(f, v.x); ST(f + 1, v.y); ST(f + 2, v.z); };
+      __builtin_amdgcn_make_buffer_rsrc(P.pstate, 0, (int)(P.nslots * kSlots * 16), kBufWord3);
+  const uint32_t pvo = ((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * (uint32_t)kSlots * 64u + (uint32_t)lane) * 16u;
+  auto LD2 = [&](int s) { return buf_ld2(prs, pvo, (uint32_t)s * 1024u); };
+  auto ST2 = [&](int s, double a, double b) { buf_st2(prs, pvo, (uint32_t)s * 1024u, a, b); };
+  auto LD1 = [&](int s) { return buf_ld(prs, pvo, (uint32_t)s * 1024u); };
+  auto ST1 = [&](int s, double a) { buf_st(prs, pvo, (uint32_t)s * 1024u, a); };
+  // a vector in slots (s, s+1): x, y in s, z in the first half of s + 1
+  auto LDV = [&](int s) { const D2 q = LD2(s); return d3(q.a, q.b, LD1(s + 1)); };
+  auto STV = [&](int s, D3 v) { ST2(s, v.x, v.y); ST1(s + 1, v.z); };
+  // the shadowable-hit record: HP, HN, HV
+  auto ST_HIT = [&](D3 p, D3 n, D3 v) {
+    ST2(S_HP01, p.x, p.y); ST2(S_HP2_HN0, p.z, n.x); ST2(S_HN12, n.y, n.z); ST2(S_HV01, v.x, v.y); ST1(S_HV2, v.z);
+  };
+  auto LD_HP = [&]() { const D2 a = LD2(S_HP01), b = LD2(S_HP2_HN0); return d3(a.a, a.b, b.a); };
+  auto LD_HN = [&]() { const D2 a = LD2(S_HP2_HN0), b = LD2(S_HN12); return d3(a.b, b.a, b.b); };
+  auto LD_HV = [&]() { return LDV(S_HV01); };
+  // colour and weight carried across mirror bounces
+  auto LD_SCOL_W = [&](D3& scol, double& w) {
+    const D2 a = LD2(S_SCOL01), b = LD2(S_SCOL2_W);
+    scol = d3(a.a, a.b, b.a);
+    w = b.b;
+  };
+  auto ST_SCOL_W = [&](D3 scol, double w) { ST2(S_SCOL01, scol.x, scol.y); ST2(S_SCOL2_W, scol.z, w); };
 
   // wave-uniform work-head cursor; in list mode the work count comes from the device
   const long long n_list = P.list ? (long long)*P.list_count * P.nsamp : 0;   // work items
@@ -601,12 +638,12 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
       };
       const D3 c3 = d3(-rd.x, -rd.y, -rd.z);
 
-      // wave-level iterations of this round; wave-uniform (SALU only), so the watchdog
-      // costs the node loop no VALU
-      uint32_t wit = 0;
-      auto trav_guard = [&]() -> bool {
-        wit = __builtin_amdgcn_readfirstlane(wit) + 1u;
-        return wit > kTravGuard;
+      // Watchdog of the traversal loops: each loop counts its own wave-level iterations in a
+      // counter that lives only inside that loop, so it stays wave-uniform (an SGPR: the check
+      // costs SALU only, no VALU in the node loop).  A loop that runs past kTravGuard
+      // iterations abandons the ray (results void) and flags the launch.
+      auto guard_trip = [&]() {
+        if (lane == __ffsll((long long)__ballot(1)) - 1) atomicOr(&P.ctr[CD_GUARD], 1ull);
       };
       // tests the triangles of leaf `lref` in record order; true = any-hit ray occluded
       auto test_leaf = [&](uint32_t lref) -> bool {
@@ -616,8 +653,8 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
           uint32_t i = lref & ~kLeaf;
           const uint32_t leaf0 = i;
           bool occluded = false;
-          for (;;) {
-            if (trav_guard()) break;
+          for (uint32_t it = 0;; ++it) {
+            if (it > kTravGuard) { guard_trip(); occluded = true; break; }
             const uint32_t rec = (WIDTH == 2) ? P.slot2dev[i] : i;
             if (STATS) {
               c_tris++;
@@ -676,17 +713,18 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
       };
       uint32_t pleaf = kDone;   // 4-wide: postponed leaf
 
+      uint32_t rounds = 0;
       while (__ballot(cur != kDone || pleaf != kDone) != 0) {
-        if (trav_guard()) {   // watchdog: abandon the round (results void, launch flagged)
-          if (lane == __ffsll((long long)__ballot(1)) - 1) atomicOr(&P.ctr[CD_GUARD], 1ull);
+        if (++rounds > kTravGuard) {   // watchdog: abandon the round (results void, launch flagged)
+          guard_trip();
           cur = kDone;
           pleaf = kDone;
           break;
         }
         if (STATS) wave_tick(d_round_it, d_round_ln, lane);
         if constexpr (WIDTH == 2) {
-        while (!(cur & kLeaf)) {   // internal node (kDone carries the leaf bit)
-          if (trav_guard()) break;
+        for (uint32_t it = 0; !(cur & kLeaf); ++it) {   // internal node (kDone carries the leaf bit)
+          if (it > kTravGuard) { guard_trip(); cur = kDone; break; }
           if (STATS) { c_nodes++; wave_tick(d_node_it, d_node_ln, lane); wave_distinct(cur, d_node_lines, lane); }
           const float4* nq = reinterpret_cast<const float4*>(P.nodes + cur);
           const float4 bx = nq[0], by = nq[1], bz = nq[2];
@@ -716,8 +754,8 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
           }
         }
         } else {
-        while (!(cur & kLeaf)) {   // 4-wide node: test 4 boxes, visit nearest, push the rest far-first
-          if (trav_guard()) break;
+        for (uint32_t it = 0; !(cur & kLeaf); ++it) {   // 4-wide node: test 4 boxes, visit nearest, push the rest far-first
+          if (it > kTravGuard) { guard_trip(); cur = kDone; pleaf = kDone; break; }
           if (STATS) { c_nodes++; wave_tick(d_node_it, d_node_ln, lane); wave_distinct(cur, d_node_lines, lane); }
           float k[4];
           uint32_t v[4];
@@ -833,10 +871,13 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
 
     // ================= SHADE phase (owners) =================
     want = 0;
+    // the hit being shaded: live from SHADE into the fan-out below (an owner that offers rays
+    // has just computed or loaded them), so the fan-out never reads back path state the wave
+    // stored in this same iteration
+    D3 hp = d3(0, 0, 0), hn = d3(0, 0, 0), hview = d3(0, 0, 0);
     if (state == ST_CLOSEST || state == ST_SHADOW) {
       bool hit_ready = (state == ST_CLOSEST), finish = false;
       D3 scol = d3(0, 0, 0);   // the sample's colour so far once the path ends (finish)
-      D3 hp, hn, hview;
       double mirror = 0.0;
       // lighting() for one light (mytracer.cpp:579-606): Lambert + Phong term of light j
       auto contrib_of = [&](int j, D3 hp_, D3 hn_, D3 hv_, D3 hd_, const GMat& M) {
@@ -869,11 +910,13 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
         want = min(rest, kBatchExtra) + ((rest <= kBatchExtra && mirror_ > 0.0 && depth < P.max_depth) ? 1 : 0);
       };
       if (state == ST_SHADOW) {   // batch finished: lights [light, batch_end) in order
-        hp = LD3(F_HP); hn = LD3(F_HN); hview = LD3(F_HVIEW);
-        const D3 hdiff = LD3(F_HDIFF);
-        mirror = LD(F_MIRROR);
-        D3 lacc = LD3(F_LACC);
+        hp = LD_HP(); hn = LD_HN(); hview = LD_HV();
         const GMat& M = P.mats[mesh];
+        const D3 hdiff = M.tex_w > 0 ? LDV(S_HD01) : d3(M.kd[0], M.kd[1], M.kd[2]);
+        mirror = M.mirror;
+        // first batch: the ambient term (mytracer.cpp:574-576) again, else the stored sum
+        D3 lacc = light == 0 ? d3(0.0 + P.amb[0] * M.ka[0], 0.0 + P.amb[1] * M.ka[1], 0.0 + P.amb[2] * M.ka[2])
+                             : LDV(S_LACC01);
         const uint32_t vw = lvis[threadIdx.x];
         for (int j = light; j < batch_end; ++j) {
           const bool occluded = (j == light) ? shadow_hit : (((vw >> (j - light)) & 1u) != 0u);
@@ -883,14 +926,15 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
         }
         light = batch_end;
         if (light < P.n_lights) {
-          ST3(F_LACC, lacc);
+          STV(S_LACC01, lacc);
           launch_batch(hp, mirror);
         } else {   // bounce complete (subtrace, mytracer.cpp:546-555)
-          const double w = depth == 0 ? 1.0 : LD(F_W);
-          scol = add(depth == 0 ? d3(0, 0, 0) : LD3(F_SCOL), scl(w, scl(1.0 - mirror, lacc)));
+          D3 s0 = d3(0, 0, 0);
+          double w = 1.0;
+          if (depth > 0) LD_SCOL_W(s0, w);
+          scol = add(s0, scl(w, scl(1.0 - mirror, lacc)));
           if (mirror > 0.0 && depth < P.max_depth) {
-            ST3(F_SCOL, scol);
-            ST(F_W, w * mirror);
+            ST_SCOL_W(scol, w * mirror);
             depth++;
             if (refl_h >= 0) {   // reflection ray traced by a helper this round
               const int ht = wbase + refl_h;
@@ -917,8 +961,10 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
       }
       if (hit_ready) {
         if (best == kNoHit) {   // miss: background (mytracer_gpu.cu:262, :292)
-          const double w = depth == 0 ? 1.0 : LD(F_W);
-          scol = add(depth == 0 ? d3(0, 0, 0) : LD3(F_SCOL), scl(w, d3(P.bg[0], P.bg[1], P.bg[2])));
+          D3 s0 = d3(0, 0, 0);
+          double w = 1.0;
+          if (depth > 0) LD_SCOL_W(s0, w);
+          scol = add(s0, scl(w, d3(P.bg[0], P.bg[1], P.bg[2])));
           finish = true;
         } else {
           if (STATS) c_hits++;
@@ -978,17 +1024,17 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
           D3 lacc = d3(0.0 + P.amb[0] * M.ka[0], 0.0 + P.amb[1] * M.ka[1], 0.0 + P.amb[2] * M.ka[2]);
           light = 0;
           if (M.shadowable && P.n_lights > 0) {   // shadow rays, mytracer.cpp:589-600
-            ST3(F_HP, hp); ST3(F_HN, hn); ST3(F_HVIEW, hview); ST3(F_HDIFF, hdiff);
-            ST(F_MIRROR, mirror);
-            ST3(F_LACC, lacc);
+            ST_HIT(hp, hn, hview);
+            if (M.tex_w > 0) STV(S_HD01, hdiff);
             launch_batch(hp, mirror);
           } else {
             for (int j = 0; j < P.n_lights; ++j) lacc = add(lacc, contrib_of(j, hp, hn, hview, hdiff, M));
-            const double w = depth == 0 ? 1.0 : LD(F_W);
-            scol = add(depth == 0 ? d3(0, 0, 0) : LD3(F_SCOL), scl(w, scl(1.0 - mirror, lacc)));
+            D3 s0 = d3(0, 0, 0);
+            double w = 1.0;
+            if (depth > 0) LD_SCOL_W(s0, w);
+            scol = add(s0, scl(w, scl(1.0 - mirror, lacc)));
             if (mirror > 0.0 && depth < P.max_depth) {
-              ST3(F_SCOL, scol);
-              ST(F_W, w * mirror);
+              ST_SCOL_W(scol, w * mirror);
               depth++;
               const D3 d = d3(-hview.x, -hview.y, -hview.z);
               const double s2 = 2.0 * dot(hn, d);
@@ -1008,10 +1054,10 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
         so[0] = c.x; so[1] = c.y; so[2] = c.z;
         state = heads_left > 0 ? ST_FETCH : ST_DONE;
       } else if (finish) {
-        const D3 pcol = add(sample == 0 ? d3(0, 0, 0) : LD3(F_PCOL), scol);
+        const D3 pcol = add(sample == 0 ? d3(0, 0, 0) : LDV(S_PCOL01), scol);
         sample++;
         if (sample < P.spp_n * P.spp_n) {
-          ST3(F_PCOL, pcol);
+          STV(S_PCOL01, pcol);
           start_sample();
         } else {   // compute_image: average, clamp, store (mytracer_gpu.cu:155-159, 221-227)
           const double nn = (double)(P.spp_n * P.spp_n);
@@ -1047,7 +1093,6 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
         const int avail = (int)__popcll(I);   // __popcll is unsigned: keep the subtraction signed
         const int got = min(want, max(0, avail - off));
         if (got > 0) {
-          const D3 hp = LD3(F_HP);
           const int n_extra_lights = min(P.n_lights - light - 1, kBatchExtra);
           for (int t = 0; t < got; ++t) {
             const int ht = wbase + kth_set_bit(I, off + t);
@@ -1064,8 +1109,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
               tw = (uint32_t)lane | ((uint32_t)(t + 1) << 8);
               c_shadow++;
             } else {   // reflection ray (same formula as the owner's own emission)
-              const D3 hn = LD3(F_HN), hv = LD3(F_HVIEW);
-              const D3 dd = d3(-hv.x, -hv.y, -hv.z);
+              const D3 dd = d3(-hview.x, -hview.y, -hview.z);
               const double s2 = 2.0 * dot(hn, dd);
               const D3 v = sub(dd, scl(s2, hn));
               o = add(hp, scl(1e-4, v));
@@ -1318,7 +1362,7 @@ struct LaunchCtx {
   unsigned long long* d_ctr = nullptr;       // [kCtrWords] work heads, stats, diagnostics, then
                                              // FrameDesc[kMaxFrames] (one H2D copy per launch)
   unsigned char* h_ctl = nullptr;            // pinned staging of the same bytes
-  double* d_pstate = nullptr;                // [nslots][kFields] path state
+  double* d_pstate = nullptr;                // path state, nslots x kSlots x 16 B
   uint32_t* d_spill = nullptr;               // [stack_words][nslots] (only when stack_words > kShortStack)
   unsigned long long* d_wavelog = nullptr;   // [nslots / 64][4]
   hipEvent_t ev0 = nullptr, ev1 = nullptr;   // kernel start / end (timing, reuse fence)
@@ -2218,10 +2262,28 @@ int rt_scene_upload(const rt_scene_soa* s, const rt_bvh_soa* b, int device, rt_s
   return rt_scene_upload_ex(s, b, device, nullptr, out);
 }
 
-int rt_scene_upload_ex(const rt_scene_soa* s, const rt_bvh_soa* b, int device, const rt_upload_options* opt,
-                       rt_scene** out) {
-  if (!out) return fail(RT_ERR_INVALID, "rt_scene_upload: null out");
-  *out = nullptr;
+}  // extern "C"
+
+namespace {
+// Host-side device layout of a scene: built once (the expensive part: device hierarchy,
+// records), then copied to any number of devices (upload_image).
+struct SceneImage {
+  std::vector<GNode> nodes;
+  std::vector<GNode4> nodes4;
+  std::vector<GTri> tris;
+  std::vector<uint32_t> slot2dev;
+  std::vector<TriShade> shade;
+  std::vector<double> tnorm, tu, tv;
+  std::vector<unsigned char> texels;
+  std::vector<GMat> mats;
+  long long n_tris = 0;
+  int n_meshes = 0;
+  int depth = 0, stack4 = 1;
+  double delta = 0.0;
+  double root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};
+};
+
+int build_image(const rt_scene_soa* s, const rt_bvh_soa* b, const rt_upload_options* opt, SceneImage& I) {
   int tree_kind = RT_TREE_SBVH;
   if (const char* e = std::getenv("RT_DEVICE_TREE"))   // process default override (A/B runs)
     tree_kind = std::strcmp(e, "reference") == 0 || std::strcmp(e, "median") == 0 ? RT_TREE_REFERENCE
@@ -2541,46 +2603,67 @@ int rt_scene_upload_ex(const rt_scene_soa* s, const rt_bvh_soa* b, int device, c
     G.tex_h = s->mesh_tex_height[m];
     G.tex_off = s->mesh_tex_offset[m];
   }
-  std::vector<double> tu(s->tex_u, s->tex_u + s->n_tex_coords), tv(s->tex_v, s->tex_v + s->n_tex_coords);
-  std::vector<unsigned char> texels(s->texels, s->texels + 3 * s->n_texels);
-
+  I.tu.assign(s->tex_u, s->tex_u + s->n_tex_coords);
+  I.tv.assign(s->tex_v, s->tex_v + s->n_tex_coords);
+  I.texels.assign(s->texels, s->texels + 3 * s->n_texels);
+  I.nodes = std::move(nodes);
+  I.nodes4 = std::move(nodes4);
+  I.tris = std::move(tris);
+  I.slot2dev = std::move(slot2dev);
+  I.shade = std::move(shade);
+  I.tnorm = std::move(tnorm);
+  I.mats = std::move(mats);
+  I.n_tris = nt;
+  I.n_meshes = s->n_meshes;
+  I.depth = depth;
+  I.stack4 = stack4;
+  I.delta = delta;
+  if (nt > 0)
+    for (int k = 0; k < 3; ++k) {
+      I.root_lo[k] = b->bb_min[k] - delta;
+      I.root_hi[k] = b->bb_max[k] + delta;
+    }
   tick("misc");
+  return RT_OK;
+}
+
+// Copies a built scene image to `device` and allocates its launch contexts.
+int upload_image(const SceneImage& I, int device, rt_scene** out) {
   HIP_TRY(hipSetDevice(device));
   auto* sc = new rt_scene();
   sc->device = device;
   long long bytes = 0;
-  rc = RT_OK;
-  if (rc == RT_OK) rc = upload(&sc->d_nodes, nodes, bytes);
-  if (rc == RT_OK) rc = upload(&sc->d_nodes4, nodes4, bytes);
-  if (rc == RT_OK) rc = upload(&sc->d_tris, tris, bytes);
-  if (rc == RT_OK) rc = upload(&sc->d_slot2dev, slot2dev, bytes);
-  if (rc == RT_OK) rc = upload(&sc->d_shade, shade, bytes);
-  if (rc == RT_OK) rc = upload(&sc->d_tnorm, tnorm, bytes);
-  if (rc == RT_OK) rc = upload(&sc->d_tu, tu, bytes);
-  if (rc == RT_OK) rc = upload(&sc->d_tv, tv, bytes);
-  if (rc == RT_OK) rc = upload(&sc->d_texels, texels, bytes);
-  if (rc == RT_OK) rc = upload(&sc->d_mats, mats, bytes);
+  int rc = RT_OK;
+  if (rc == RT_OK) rc = upload(&sc->d_nodes, I.nodes, bytes);
+  if (rc == RT_OK) rc = upload(&sc->d_nodes4, I.nodes4, bytes);
+  if (rc == RT_OK) rc = upload(&sc->d_tris, I.tris, bytes);
+  if (rc == RT_OK) rc = upload(&sc->d_slot2dev, I.slot2dev, bytes);
+  if (rc == RT_OK) rc = upload(&sc->d_shade, I.shade, bytes);
+  if (rc == RT_OK) rc = upload(&sc->d_tnorm, I.tnorm, bytes);
+  if (rc == RT_OK) rc = upload(&sc->d_tu, I.tu, bytes);
+  if (rc == RT_OK) rc = upload(&sc->d_tv, I.tv, bytes);
+  if (rc == RT_OK) rc = upload(&sc->d_texels, I.texels, bytes);
+  if (rc == RT_OK) rc = upload(&sc->d_mats, I.mats, bytes);
   if (rc != RT_OK) {
     rt_scene_free(sc);
     return rc;
   }
-  sc->n_gnodes = (int)nodes.size();
-  sc->n_tris = nt;
-  sc->n_meshes = s->n_meshes;
-  sc->mesh_mats = mats;
-  sc->table_bytes = (long long)(std::max<size_t>(mats.size(), 1) * sizeof(GMat));
-  sc->depth = depth;
-  sc->stack_words = std::max(std::max(1, depth), stack4);
-  sc->n_gnodes4 = (int)nodes4.size();
+  sc->n_gnodes = (int)I.nodes.size();
+  sc->n_tris = I.n_tris;
+  sc->n_meshes = I.n_meshes;
+  sc->mesh_mats = I.mats;
+  sc->table_bytes = (long long)(std::max<size_t>(I.mats.size(), 1) * sizeof(GMat));
+  sc->depth = I.depth;
+  sc->stack_words = std::max(std::max(1, I.depth), I.stack4);
+  sc->n_gnodes4 = (int)I.nodes4.size();
   sc->n_top = RT_TOP_NODES > 0 ? std::min(kTopNodes, sc->n_gnodes4) : 0;
   if (const char* e = std::getenv("RT_LDS_TOP"))   // A/B knob: cache fewer nodes (0 = none)
     sc->n_top = std::max(0, std::min(sc->n_top, std::atoi(e)));
-  sc->delta = delta;
-  if (nt > 0)
-    for (int k = 0; k < 3; ++k) {
-      sc->root_lo[k] = b->bb_min[k] - delta;
-      sc->root_hi[k] = b->bb_max[k] + delta;
-    }
+  sc->delta = I.delta;
+  for (int k = 0; k < 3; ++k) {
+    sc->root_lo[k] = I.root_lo[k];
+    sc->root_hi[k] = I.root_hi[k];
+  }
   sc->bytes = bytes;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) { rt_scene_free(sc); return fail(RT_ERR_HIP, "hipGetDeviceProperties failed"); }
@@ -2603,7 +2686,7 @@ int rt_scene_upload_ex(const rt_scene_soa* s, const rt_bvh_soa* b, int device, c
   sc->light_cap = RT_MAX_LIGHTS;
   sc->bytes += (long long)(RT_MAX_LIGHTS * 6 * sizeof(double));
   for (LaunchCtx& c : sc->ctx) {
-    const size_t pb = sc->nslots * kFields * sizeof(double);
+    const size_t pb = sc->nslots * kSlots * 16;
     const size_t wb = sc->nslots / 64 * 4 * sizeof(unsigned long long);
     const size_t sb = sc->stack_words > kShortStack ? sc->nslots * (size_t)sc->stack_words * sizeof(uint32_t) : 0;
     if (hipMalloc(reinterpret_cast<void**>(&c.d_ctr), kCtlBytes) != hipSuccess ||
@@ -2619,6 +2702,46 @@ int rt_scene_upload_ex(const rt_scene_soa* s, const rt_bvh_soa* b, int device, c
     sc->bytes += (long long)(kCtlBytes + pb + wb + sb);
   }
   *out = sc;
+  return RT_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int rt_scene_upload_ex(const rt_scene_soa* s, const rt_bvh_soa* b, int device, const rt_upload_options* opt,
+                       rt_scene** out) {
+  if (!out) return fail(RT_ERR_INVALID, "rt_scene_upload: null out");
+  *out = nullptr;
+  SceneImage I;
+  const int rc = build_image(s, b, opt, I);
+  return rc != RT_OK ? rc : upload_image(I, device, out);
+}
+
+int rt_scene_upload_multi(const rt_scene_soa* s, const rt_bvh_soa* b, const int* devices, int n_devices,
+                          const rt_upload_options* opt, rt_scene** outs) {
+  if (!outs || !devices || n_devices < 1) return fail(RT_ERR_INVALID, "rt_scene_upload_multi: bad argument");
+  for (int g = 0; g < n_devices; ++g) outs[g] = nullptr;
+  SceneImage I;
+  int rc = build_image(s, b, opt, I);
+  if (rc != RT_OK) return rc;
+  // one host thread per device: the copies and context allocations proceed in parallel
+  std::vector<int> rcs(n_devices, RT_OK);
+  std::vector<std::string> errs(n_devices);
+  std::vector<std::thread> th;
+  for (int g = 0; g < n_devices; ++g)
+    th.emplace_back([&, g]() {
+      rcs[g] = upload_image(I, devices[g], &outs[g]);
+      if (rcs[g] != RT_OK) errs[g] = g_error;   // thread-local message of that thread
+    });
+  for (auto& t : th) t.join();
+  for (int g = 0; g < n_devices; ++g)
+    if (rcs[g] != RT_OK) {
+      for (int k = 0; k < n_devices; ++k) {
+        rt_scene_free(outs[k]);
+        outs[k] = nullptr;
+      }
+      return fail(rcs[g], "rt_scene_upload_multi: device " + std::to_string(devices[g]) + ": " + errs[g]);
+    }
   return RT_OK;
 }
 

@@ -7,7 +7,9 @@
 //
 //   rt_render --scene office|cornell|random_tris|spheres|path.sce
 //             [--width W --height H --spp N --max-depth D --tris N --seed S
-//              --detail K --device I --frames F --out image.ppm]
+//              --detail K --device I --gpus N --frames F --out image.ppm]
+// --gpus N renders each frame on GPUs 0..N-1 (row stripes + one RCCL gather, rt_multi.h);
+// without it one device (--device) renders through rt_launch_compute_image.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -17,17 +19,19 @@
 
 #include "../../../include/rt_hip.h"
 #include "../../../include/rt_host.h"
+#include "../../../include/rt_multi.h"
 
 namespace {
 
 class Raytracer {
  public:
   ~Raytracer() {
+    rt_multi_free(multi_);
     rt_scene_free(gpu_);
     rt_host_free(host_);
   }
-  // Raytracer::init_cuda equivalent.
-  bool init(const std::string& scene, const rt_gen_params& gp, int device) {
+  // Raytracer::init_cuda equivalent; gpus >= 1: every frame sharded over GPUs 0..gpus-1.
+  bool init(const std::string& scene, const rt_gen_params& gp, int device, int gpus) {
     int rc = (scene.size() > 4 && scene.substr(scene.size() - 4) == ".sce") ? rt_host_load(scene.c_str(), &host_)
                                                                               : rt_host_generate(scene.c_str(), &gp, &host_);
     if (rc != RT_OK) return error(rt_host_last_error());
@@ -35,6 +39,14 @@ class Raytracer {
     if (rt_host_prepare(host_, &build_s) != RT_OK) return error(rt_host_last_error());
     std::printf("scene %s: %lld triangles, BVH depth %d, host build %.3f s\n", scene.c_str(),
                 rt_host_triangle_count(host_), rt_host_bvh_depth(host_), build_s);
+    if (gpus >= 1) {
+      std::vector<int> devs(gpus);
+      for (int g = 0; g < gpus; ++g) devs[g] = g;
+      if (rt_multi_create(rt_host_soa(host_), rt_host_bvh(host_), devs.data(), gpus, nullptr, &multi_) != RT_OK)
+        return error(rt_multi_last_error());
+      std::printf("uploaded to %d devices (row stripes of %d rows, RCCL gather to device 0)\n", gpus, kStripe);
+      return true;
+    }
     if (rt_scene_upload(rt_host_soa(host_), rt_host_bvh(host_), device, &gpu_) != RT_OK) return error(rt_last_error());
     std::printf("uploaded %.1f MB to device %d\n", rt_scene_device_bytes(gpu_) / 1e6, device);
     return true;
@@ -46,9 +58,16 @@ class Raytracer {
     image_.assign(3 * (size_t)params_.camera.width * params_.camera.height, 0.f);
     for (int f = 0; f < frames; ++f) {
       rt_stats st;
-      if (rt_render_to_host(gpu_, &params_, image_.data(), &st) != RT_OK) return error(rt_last_error());
       float ms = 0;
-      rt_last_kernel_ms(gpu_, &ms);
+      if (multi_) {
+        double mt = 0;
+        if (rt_multi_render_to_host(multi_, &params_, kStripe, image_.data(), &st, &mt) != RT_OK)
+          return error(rt_multi_last_error());
+        ms = (float)mt;
+      } else {
+        if (rt_render_to_host(gpu_, &params_, image_.data(), &st) != RT_OK) return error(rt_last_error());
+        rt_last_kernel_ms(gpu_, &ms);
+      }
       const long long rays = st.primary_rays + st.shadow_rays + st.reflection_rays;
       std::printf("frame %d: %dx%d spp %d  kernel %.3f ms  rays %lld (P %lld S %lld R %lld)  %.1f Mrays/s\n", f,
                   params_.camera.width, params_.camera.height, params_.spp_n * params_.spp_n, ms, rays,
@@ -68,8 +87,10 @@ class Raytracer {
     std::fprintf(stderr, "rt_render: %s\n", msg);
     return false;
   }
+  static constexpr int kStripe = 16;   // rows per stripe (interleaved over the GPUs)
   rt_host_scene* host_ = nullptr;
   rt_scene* gpu_ = nullptr;
+  rt_multi* multi_ = nullptr;
   rt_render_params params_{};
   std::vector<float> image_;
 };
@@ -78,7 +99,7 @@ class Raytracer {
 
 int main(int argc, char** argv) {
   std::string scene = "office", out;
-  int width = 0, height = 0, spp = 1, max_depth = -1, device = 0, frames = 1;
+  int width = 0, height = 0, spp = 1, max_depth = -1, device = 0, frames = 1, gpus = 0;
   rt_gen_params gp{};
   gp.max_depth = -1;
   for (int i = 1; i < argc; ++i) {
@@ -97,11 +118,13 @@ int main(int argc, char** argv) {
     else if (a == "--detail") gp.detail = std::atoi(next());
     else if (a == "--device") device = std::atoi(next());
     else if (a == "--frames") frames = std::atoi(next());
+    else if (a == "--gpus") gpus = std::atoi(next());
     else if (a == "--out") out = next();
     else { std::fprintf(stderr, "unknown option %s\n", a.c_str()); return 2; }
   }
   Raytracer rt;
-  if (!rt.init(scene, gp, device)) return 1;
+  if (gpus < 0) { std::fprintf(stderr, "--gpus must be >= 1\n"); return 2; }
+  if (!rt.init(scene, gp, device, gpus)) return 1;
   if (!rt.compute_image(width, height, spp, max_depth, frames)) return 1;
   if (!out.empty() && !rt.write(out)) return 1;
   return 0;

@@ -22,9 +22,11 @@ PKG_ROOT = Path(__file__).resolve().parent.parent
 LIB_DIR = PKG_ROOT / "lib"
 HOST_LIB = LIB_DIR / "librt_host.so"
 HIP_LIB = Path(os.environ.get("RTAMD_HIP_LIB", LIB_DIR / "librt_hip.so"))   # override: kernel variants
+MULTI_LIB = LIB_DIR / "librt_multi.so"
 
 _host = None
 _hip = None
+_multi = None
 
 
 class RtError(RuntimeError):
@@ -47,6 +49,17 @@ def hip_lib():
             raise RtError(f"{HIP_LIB} not built: run `make -C my-raytracer_amd` or __graft_entry__.build()")
         _hip = abi.bind(C.CDLL(str(HIP_LIB)), abi.HIP_SYMBOLS)
     return _hip
+
+
+def multi_lib():
+    """librt_multi.so (include/rt_multi.h): the single-process multi-GPU driver (RCCL)."""
+    global _multi
+    if _multi is None:
+        if not MULTI_LIB.exists():
+            raise RtError(f"{MULTI_LIB} not built: run `make -C my-raytracer_amd` or __graft_entry__.build()")
+        hip_lib()   # librt_multi links librt_hip: load the same copy first
+        _multi = abi.bind(C.CDLL(str(MULTI_LIB)), abi.MULTI_SYMBOLS)
+    return _multi
 
 
 def _check_host(rc, what):
@@ -364,6 +377,56 @@ def write_ppm(path, img):
     h, w, _ = img.shape
     _check_host(host_lib().rt_write_ppm(str(path).encode(), img.ctypes.data_as(C.POINTER(C.c_float)), w, h),
                 "rt_write_ppm")
+
+
+class MultiScene:
+    """One scene on several GPUs of this node, one process (rt_multi.h): every frame is cut
+    into interleaved row stripes per GPU and assembled on devices[0] by one RCCL gather."""
+
+    def __init__(self, host_scene, devices=(0,), tree=None):
+        self._h = C.c_void_p()
+        devs = (C.c_int * len(devices))(*devices)
+        opt = None
+        if tree is not None:
+            kinds = {"sah": abi.RT_TREE_SAH, "reference": abi.RT_TREE_REFERENCE, "sbvh": abi.RT_TREE_SBVH}
+            opt = C.byref(abi.UploadOptions(device_tree=kinds[tree]))
+        rc = multi_lib().rt_multi_create(host_scene.soa, host_scene.bvh, devs, len(devices), opt, C.byref(self._h))
+        if rc != RT_OK:
+            raise RtError(f"rt_multi_create: {multi_lib().rt_multi_last_error().decode()}")
+        self.devices = tuple(devices)
+
+    def render(self, params, stripe_height=16):
+        """Synchronous render of the whole frame to host memory -> (image [H, W, 3], Stats, ms)."""
+        dt = np.float64 if params.out_format == RT_OUT_RGB_F64 else np.float32
+        img = np.zeros((params.camera.height, params.camera.width, 3), dtype=dt)
+        st, ms = abi.Stats(), C.c_double()
+        rc = multi_lib().rt_multi_render_to_host(self._h, C.byref(params), stripe_height, img.ctypes.data_as(C.c_void_p),
+                                                 C.byref(st), C.byref(ms))
+        if rc != RT_OK:
+            raise RtError(f"rt_multi_render: {multi_lib().rt_multi_last_error().decode()}")
+        return img, st, ms.value
+
+    def close(self):
+        if self._h:
+            multi_lib().rt_multi_free(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def multi_interleave_host(gathered, height, stripe_height, n):
+    """Host restatement of rt_multi's frame assembly: gathered [n, max_rows, W, C] -> [H, W, C]."""
+    g = np.ascontiguousarray(gathered)
+    out = np.empty((height,) + g.shape[2:], dtype=g.dtype)
+    rc = multi_lib().rt_multi_interleave_host(g.ctypes.data_as(C.c_void_p), out.ctypes.data_as(C.c_void_p), height,
+                                              g.shape[2], g.shape[3], g.itemsize, stripe_height, n)
+    if rc != RT_OK:
+        raise RtError(f"rt_multi_interleave_host: {multi_lib().rt_multi_last_error().decode()}")
+    return out
 
 
 class Raytracer:

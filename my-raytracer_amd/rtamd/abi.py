@@ -143,6 +143,8 @@ HIP_SYMBOLS = {
     "rt_scene_upload": (C.c_int, [C.POINTER(SceneSoA), C.POINTER(BvhSoA), C.c_int, C.POINTER(C.c_void_p)]),
     "rt_scene_upload_ex": (C.c_int, [C.POINTER(SceneSoA), C.POINTER(BvhSoA), C.c_int, C.POINTER(UploadOptions),
                                      C.POINTER(C.c_void_p)]),
+    "rt_scene_upload_multi": (C.c_int, [C.POINTER(SceneSoA), C.POINTER(BvhSoA), C.POINTER(C.c_int), C.c_int,
+                                        C.POINTER(UploadOptions), C.POINTER(C.c_void_p)]),
     "rt_scene_set_analytic": (C.c_int, [C.c_void_p, C.POINTER(Sphere), C.c_int, C.POINTER(Plane), C.c_int]),
     "rt_scene_device_bytes": (C.c_longlong, [C.c_void_p]),
     "rt_rows_in_shard": (C.c_int, [C.POINTER(RenderParams)]),
@@ -180,6 +182,22 @@ HOST_SYMBOLS = {
     "rt_host_bvh_depth": (C.c_int, [C.c_void_p]),
     "rt_host_free": (None, [C.c_void_p]),
     "rt_host_last_error": (C.c_char_p, []),
+}
+
+
+MULTI_SYMBOLS = {
+    "rt_multi_create": (C.c_int, [C.POINTER(SceneSoA), C.POINTER(BvhSoA), C.POINTER(C.c_int), C.c_int,
+                                  C.POINTER(UploadOptions), C.POINTER(C.c_void_p)]),
+    "rt_multi_device_count": (C.c_int, [C.c_void_p]),
+    "rt_multi_render": (C.c_int, [C.c_void_p, C.POINTER(RenderParams), C.c_int, C.c_void_p, C.POINTER(Stats),
+                                  C.POINTER(C.c_double)]),
+    "rt_multi_render_to_host": (C.c_int, [C.c_void_p, C.POINTER(RenderParams), C.c_int, C.c_void_p,
+                                          C.POINTER(Stats), C.POINTER(C.c_double)]),
+    "rt_multi_max_rows": (C.c_int, [C.c_int, C.c_int, C.c_int]),
+    "rt_multi_interleave_host": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                           C.c_int]),
+    "rt_multi_free": (None, [C.c_void_p]),
+    "rt_multi_last_error": (C.c_char_p, []),
 }
 
 

@@ -25,7 +25,8 @@ def exported(lib):
     return {line.split()[-1] for line in out.splitlines() if line.split()}
 
 
-@pytest.mark.parametrize("header,lib", [("rt_hip.h", rtamd.HIP_LIB), ("rt_host.h", rtamd.HOST_LIB)])
+@pytest.mark.parametrize("header,lib", [("rt_hip.h", rtamd.HIP_LIB), ("rt_host.h", rtamd.HOST_LIB),
+                                        ("rt_multi.h", rtamd.MULTI_LIB)])
 def test_every_declared_symbol_exported(header, lib):
     syms = declared(header)
     assert syms, header
@@ -36,6 +37,8 @@ def test_every_declared_symbol_exported(header, lib):
 def test_ctypes_tables_cover_headers():
     assert set(declared("rt_hip.h")) == set(abi.HIP_SYMBOLS)
     assert set(declared("rt_host.h")) == set(abi.HOST_SYMBOLS)
+    assert set(declared("rt_multi.h")) == set(abi.MULTI_SYMBOLS)
+    rtamd.multi_lib()   # loads (and binds every symbol) without a GPU
 
 
 def test_libraries_load_and_report():

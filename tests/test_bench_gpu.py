@@ -18,6 +18,24 @@ def _gpu(gpu_available):
     return gpu_available
 
 
+SWEEP = 0.12
+
+
+def expected_frames(w, h, frames):
+    """The bench's animation path (rtamd.camera_orbit over each launch's frames): the last
+    frame it saves and the mean rays per frame of one launch, rendered here directly."""
+    hs = rtamd.HostScene.generate("office")
+    hs.prepare()
+    dev = rtamd.DeviceScene(hs, 0)
+    p = hs.render_params(w, h, 1)
+    cams = [rtamd.camera_orbit(p, SWEEP * (f / (frames - 1) - 0.5)) for f in range(frames)] if frames > 1 else [p]
+    rays, img = 0, None
+    for c in cams:
+        img, st = dev.render(c)
+        rays += st.primary_rays + st.shadow_rays + st.reflection_rays
+    return img, rays // len(cams)
+
+
 @pytest.mark.parametrize("frames", [1, 8])
 def test_bench_json_contract_and_saved_frame(tmp_path, frames):
     out = tmp_path / "frame.npy"
@@ -33,11 +51,12 @@ def test_bench_json_contract_and_saved_frame(tmp_path, frames):
     assert d["config"]["frames_per_launch"] == frames
     rf = d["roofline"]
     assert rf["bound"] == "hbm" and rf["peak"] == 8000.0 and rf["kernel_ms_avg"] > 0
-    hs = rtamd.HostScene.generate("office")
-    hs.prepare()
-    ref, st = rtamd.DeviceScene(hs, 0).render(hs.render_params(320, 180, 1))
+    assert rf["frac"] is None or 0.0 < rf["frac"] <= 1.0
+    sf = d["single_frame"]
+    assert sf["frames"] == 16 and sf["ms_per_frame"] > 0 and sf["value"] > 0
+    ref, rays = expected_frames(320, 180, frames)
     assert np.array_equal(np.load(out), ref)
-    assert d["config"]["rays_per_frame"] == st.primary_rays + st.shadow_rays + st.reflection_rays
+    assert d["config"]["rays_per_frame"] == rays
 
 
 def test_bench_adaptive_pass_runs():
@@ -71,8 +90,6 @@ def test_bench_two_ranks_rehearsal(tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     d = json.loads(r.stdout.strip().splitlines()[-1])
     assert d["n_gpus"] == 2 and d["config"]["launches_in_flight"] == 2 and d["value"] > 0
-    hs = rtamd.HostScene.generate("office")
-    hs.prepare()
-    ref, st = rtamd.DeviceScene(hs, 0).render(hs.render_params(320, 180, 1))
+    ref, rays = expected_frames(320, 180, 8)
     assert np.array_equal(np.load(out), ref)
-    assert d["config"]["rays_per_frame"] == st.primary_rays + st.shadow_rays + st.reflection_rays
+    assert d["config"]["rays_per_frame"] == rays
