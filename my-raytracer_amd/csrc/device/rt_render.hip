@@ -2866,7 +2866,10 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   P.top_off = (int)lds_bytes(sc->stack_words);
   P.lights_off = P.top_off + sc->n_top * (int)sizeof(GNode4);
   const long long waves_needed = (P.n_tiles * 64 + 63) / 64;
-  long long blocks = (long long)sc->n_cu * sc->blocks_per_cu[v];
+  int bpc = sc->blocks_per_cu[v];
+  if (const char* e = std::getenv("RT_BLOCKS_PER_CU"))   // A/B knob: a smaller persistent grid
+    bpc = std::max(1, std::min(bpc, std::atoi(e)));
+  long long blocks = (long long)sc->n_cu * bpc;
   blocks = std::max<long long>(1, std::min<long long>(blocks, (waves_needed + kBlock / 64 - 1) / (kBlock / 64)));
   blocks = std::min<long long>(blocks, (long long)(sc->nslots / kBlock));
 

@@ -42,9 +42,20 @@ def host_lib():
     return _host
 
 
+def _one_hip_runtime():
+    """PyTorch-ROCm ships its own HIP runtime (torch/lib/libamdhip64.so).  Load it before our
+    libraries so that they bind to it: a process holding both that copy and /opt/rocm's
+    (ours loaded first, torch imported later) sees no devices in one of them."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def hip_lib():
     global _hip
     if _hip is None:
+        _one_hip_runtime()
         if not HIP_LIB.exists():
             raise RtError(f"{HIP_LIB} not built: run `make -C my-raytracer_amd` or __graft_entry__.build()")
         _hip = abi.bind(C.CDLL(str(HIP_LIB)), abi.HIP_SYMBOLS)

@@ -254,24 +254,34 @@ def test_full_size_4k_16spp_sampled_rows():
     assert np.abs(img[ys].reshape(-1, 3) - ref).max() <= TOL64
 
 
-def test_config4_10m_random_triangles_sampled_pixels():
+def test_config4_10m_random_triangles_full_frame():
     # BASELINE config 4: 10 M random triangles (deep tree: depth 23, 4-wide stack bound 40 >
-    # the 16-entry LDS ring, so the global spill path runs), 1920x1080 1 spp.  Whole-frame ray
-    # counts against the kernel's own stripes; sampled pixels + their counts against the oracle.
+    # the 16-entry LDS ring, so the global spill path runs), 1920x1080 1 spp.  The WHOLE frame
+    # and its exact ray counts against the oracle's ordered traversal (the GPU algorithm's
+    # replica, which equals the reference-semantics traversal pixel for pixel:
+    # test_oracle_modes.py), plus 8000 hit-heavy pixels against the reference-semantics mode
+    # itself; the every-8th-row stripe shard's counts against the oracle's on the same pixels.
     hs, dev, orc = Case.get("random_tris", n_triangles=10_000_000)
     assert hs.bvh_depth >= 20
     p = hs.render_params(1920, 1080, 1)
     p.out_format = rtamd.RT_OUT_RGB_F64
     img, st = dev.render(p)
-    assert st.primary_rays == 1920 * 1080
+    ref, cnt = orc.render(p, pyoracle.MODE_ORDERED, threads=0)
+    assert np.abs(img - ref).max() <= TOL64
+    assert counts(st) == [cnt.primary_rays, cnt.shadow_rays, cnt.reflection_rays]
     rng = np.random.default_rng(3)
-    xy = np.stack([rng.integers(0, 1920, 400), rng.integers(0, 1080, 400)], 1).astype(np.int32)
-    xy[:100] = np.stack([rng.integers(760, 1160, 100), rng.integers(340, 740, 100)], 1)   # centre: hits
-    ref, cnt = orc.render_pixels(p, xy, pyoracle.MODE_REFERENCE)
-    got = img[xy[:, 1], xy[:, 0]]
-    assert np.abs(got - ref).max() <= TOL64
-    assert (ref.sum(-1) > 0).sum() > 50            # the sample really exercises hits and shadows
-    p.flags = rtamd.RT_FLAG_WIDE_STATS
+    xy = np.stack([rng.integers(640, 1280, 8000), rng.integers(240, 840, 8000)], 1).astype(np.int32)
+    ref2, _ = orc.render_pixels(p, xy, pyoracle.MODE_REFERENCE)
+    assert np.abs(img[xy[:, 1], xy[:, 0]] - ref2).max() <= TOL64
+    assert (ref2.sum(-1) > 0).sum() > 4000         # the sample really exercises hits and shadows
+    p.stripe_height, p.stripe_count, p.stripe_index = 1, 8, 0
+    img8, st8 = dev.render(p)
+    assert np.array_equal(img8, img[0::8])
+    ys = np.arange(0, 1080, 8)
+    xy8 = np.stack(np.meshgrid(np.arange(1920), ys), -1).reshape(-1, 2).astype(np.int32)
+    _, c8 = orc.render_pixels(p, xy8, pyoracle.MODE_ORDERED)
+    assert counts(st8) == [c8.primary_rays, c8.shadow_rays, c8.reflection_rays]
+    p.stripe_count, p.stripe_index, p.flags = 1, 0, rtamd.RT_FLAG_WIDE_STATS
     _, _ = dev.render(p)
     assert dev.debug_counters()["stack_spills"] > 0
 

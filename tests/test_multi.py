@@ -1,0 +1,102 @@
+"""Single-process multi-GPU driver (include/rt_multi.h, librt_multi.so).
+
+CPU: the row partition and the frame assembly.  Every shard of n is rendered by the CPU
+oracle with the same stripe parameters the driver gives GPU g, padded to the common
+height as ncclGather receives them, and re-interleaved by the library's host restatement
+of the assembly kernel (same index map); the result must equal the oracle's full frame
+bit for bit.  GPU: the driver itself through RCCL on the one device of the box (a one-rank
+ncclGather; RCCL refuses two ranks on one GPU, so N > 1 runs only on a multi-GPU node)
+against the single-device launch, and the CLI's --gpus path.
+"""
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import pyoracle
+import rtamd
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+@pytest.fixture(scope="module")
+def office():
+    hs = rtamd.HostScene.generate("office")
+    hs.prepare()
+    return hs, pyoracle.Oracle(hs.raw, hs)
+
+
+@pytest.mark.parametrize("h,sh,n", [(1080, 16, 8), (37, 16, 8), (45, 4, 3), (27, 1, 2), (20, 16, 1), (9, 2, 4)])
+def test_max_rows_matches_partition(h, sh, n):
+    rows = [len(rtamd.shard_rows(h, sh, n, g)) for g in range(n)]
+    assert rtamd.multi_lib().rt_multi_max_rows(h, sh, n) == max(rows)
+    assert sum(rows) == h
+
+
+@pytest.mark.parametrize("w,h,sh,n", [(48, 27, 4, 3), (40, 23, 1, 2), (32, 18, 16, 8), (24, 14, 2, 1)])
+def test_stripes_gathered_and_interleaved_equal_full_frame(office, w, h, sh, n):
+    hs, orc = office
+    full, cnt = orc.render(hs.render_params(w, h, 1), pyoracle.MODE_REFERENCE)
+    mr = rtamd.multi_lib().rt_multi_max_rows(h, sh, n)
+    gathered = np.full((n, mr, w, 3), np.nan)   # padding rows must never reach the frame
+    rays = 0
+    for g in range(n):
+        p = hs.render_params(w, h, 1)
+        p.stripe_height, p.stripe_count, p.stripe_index = sh, n, g
+        shard, c = orc.render(p, pyoracle.MODE_REFERENCE)
+        gathered[g, :shard.shape[0]] = shard
+        rays += c.primary_rays + c.shadow_rays + c.reflection_rays
+    img = rtamd.multi_interleave_host(gathered, h, sh, n)
+    assert np.array_equal(img, full)
+    assert rays == cnt.primary_rays + cnt.shadow_rays + cnt.reflection_rays
+
+
+def test_interleave_rejects_bad_arguments():
+    g = np.zeros((2, 3, 4, 3), np.float32)
+    with pytest.raises(rtamd.RtError):
+        rtamd.multi_interleave_host(g, 5, 0, 2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fmt", [rtamd.RT_OUT_RGB_F64, rtamd.RT_OUT_RGB_F32])
+def test_multi_driver_one_gpu_equals_single_launch(gpu_available, office, fmt):
+    hs, _ = office
+    m = rtamd.MultiScene(hs, devices=(0,))
+    dev = rtamd.DeviceScene(hs, 0)
+    for w, h, sh in [(320, 180, 16), (97, 61, 4)]:
+        p = hs.render_params(w, h, 1)
+        p.out_format = fmt
+        img, st, ms = m.render(p, stripe_height=sh)
+        ref, rst = dev.render(p)
+        assert np.array_equal(img, ref)
+        assert [st.primary_rays, st.shadow_rays, st.reflection_rays] == \
+            [rst.primary_rays, rst.shadow_rays, rst.reflection_rays]
+        assert ms > 0
+    m.close()
+
+
+@pytest.mark.gpu
+def test_multi_driver_rejects_duplicate_devices(gpu_available, office):
+    hs, _ = office
+    with pytest.raises(rtamd.RtError, match="distinct"):
+        rtamd.MultiScene(hs, devices=(0, 0))
+
+
+@pytest.mark.gpu
+def test_cli_gpus_path_pixels(gpu_available, tmp_path, office):
+    hs, orc = office
+    out = tmp_path / "m.ppm"
+    r = subprocess.run([str(ROOT / "my-raytracer_amd/bin/rt_render"), "--scene", "office", "--width", "96",
+                        "--height", "54", "--gpus", "1", "--out", str(out)], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert "RCCL gather" in r.stdout and "Mrays/s" in r.stdout
+    data = out.read_bytes()
+    head = b"P6\n96 54\n255\n"
+    assert data.startswith(head)
+    got = np.frombuffer(data[len(head):], np.uint8).reshape(54, 96, 3).astype(int)
+    ref, _ = orc.render(hs.render_params(96, 54, 1), pyoracle.MODE_REFERENCE)
+    want = np.floor(np.clip(ref[::-1].astype(np.float32), 0, 1) * np.float32(255) + 0.5).astype(int)
+    diff = np.abs(got - want)
+    assert diff.max() <= 1 and (diff == 0).mean() >= 0.999
