@@ -71,10 +71,20 @@ constexpr int kShortStack = RT_SHORT_STACK;
 // into each block's LDS; a node iteration whose active lanes all sit in the treelet reads
 // LDS instead of the vector-L1 path.  0 disables.
 #ifndef RT_TOP_NODES
-#define RT_TOP_NODES (RT_BLOCK / 4 - 6)   // fills the CU's 160 KB at 16 waves with the slots and the lights
+#define RT_TOP_NODES (RT_BLOCK / 4 - 7)   // fills the CU's 160 KB at 16 waves with the slots, lights and pool
 #endif
 constexpr int kTopNodes = RT_TOP_NODES > 0 ? RT_TOP_NODES : 1;
 constexpr int kStackMask = kShortStack - 1;
+// Tail compaction: once the work queue is empty, a wave with at most kDonateMax
+// pixels in flight hands them to the other waves of its block and exits, so the last pixels
+// of a launch run in fewer, fuller waves.  A handed-over lane's registers travel through the
+// donor thread's LDS stack entries (free between traversals): kMigWords words.
+#ifndef RT_DONATE_MAX
+#define RT_DONATE_MAX 24
+#endif
+constexpr int kDonateMax = RT_DONATE_MAX;
+constexpr int kMigWords = 15;
+constexpr int kPoolBytes = 64;   // LDS: live-wave count + one 64-bit lane mask per wave of the block
 static_assert((kShortStack & kStackMask) == 0, "RT_SHORT_STACK must be a power of two");
 
 // Lane states.  Owners carry a pixel (CLOSEST: closest-hit ray in flight; SHADOW: a
@@ -106,18 +116,6 @@ __device__ __forceinline__ double buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t voff
 }
 __device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, double x) {
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, x), r, voff, soff, 0);
-}
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-struct D2 {
-  double a, b;
-};
-__device__ __forceinline__ D2 buf_ld2(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-  const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
-  return D2{__builtin_bit_cast(double, u32x2_t{v.x, v.y}), __builtin_bit_cast(double, u32x2_t{v.z, v.w})};
-}
-__device__ __forceinline__ void buf_st2(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, double a, double b) {
-  const u32x2_t x = __builtin_bit_cast(u32x2_t, a), y = __builtin_bit_cast(u32x2_t, b);
-  __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{x.x, x.y, y.x, y.y}, r, voff, soff, 0);
 }
 
 
@@ -169,7 +167,7 @@ struct KParams {
   const unsigned char* texels;
   const GMat* mats;
   unsigned long long* ctr;
-  double* pstate;       // path state, [nslots / 64][kSlots][64] x 16 B
+  double* pstate;       // path state, [nslots / 64][kFields][64] fp64
   uint32_t* spill;      // [stack_words][nslots] traversal-stack entries below the LDS ring
   unsigned long long* wavelog;  // STATS: per wave {start, last refill, end, pixels} (s_memrealtime)
   const double* lights; // [n_lights][6] position xyz, colour rgb
@@ -199,6 +197,7 @@ struct KParams {
   // frames of this launch (rt_launch_frames): work item w belongs to frame w / (64 * frame_tiles)
   int n_frames;
   int lights_off;           // LDS byte offset of the lights copy ([n_lights][6] doubles)
+  int pool_off;             // LDS byte offset of the compaction pool (kPoolBytes)
   long long frame_tiles;
   const FrameDesc* frames;  // [n_frames]
 };
@@ -319,20 +318,21 @@ __device__ __forceinline__ TriOps load_tri(const GTri* tris, uint32_t i) {
   return T;
 }
 
-// Path state kept in global memory between a lane's rays, in 16-B slots (two fp64 each),
-// wave-interleaved [wave][slot][64 lanes][2]: one slot access of a wave is one b128 buffer
-// instruction over 1 KB of contiguous lines.  Only what cannot be recomputed is kept:
-//   hit point / normal / view vector of the bounce being shaded (HP, HN, HV: 9 fp64, the
-//     record of every shadowable hit -- 4 b128 + 1 b64 stores, the same loads back);
+// Path state kept in global memory between a lane's rays, wave-interleaved
+// [wave][field][64 lanes] fp64: one field access of a wave is one b64 buffer instruction over
+// 512 contiguous bytes.  Only what cannot be recomputed is kept:
+//   hit point / normal / view vector of the bounce being shaded (HP, HN, HV: the record of
+//     every shadowable hit, read back when its shadow batch completes);
 //   the textured diffuse colour (HD; untextured hits re-read the material's kd);
-//   the light sum across shadow batches (LACC; a bounce whose lights fit one batch
-//     restarts from the recomputed ambient term);
+//   the light sum across shadow batches (LACC; a bounce whose lights fit one batch restarts
+//     from the recomputed ambient term);
 //   the sample's colour and weight across mirror bounces (SCOL, W) and the pixel's sum
 //     across samples (PCOL).
-// The mirror coefficient comes from the material (the lane keeps the mesh id).
+// The mirror coefficient comes from the material (the lane keeps the mesh id).  (16-B slots
+// with b128 accesses were tried: no faster, and some pixels of mirror chains read stale
+// path state under some code layouts -- DESIGN.md §4.)
 enum : int {
-  S_HP01 = 0, S_HP2_HN0, S_HN12, S_HV01, S_HV2, S_SCOL01, S_SCOL2_W, S_PCOL01, S_PCOL2, S_HD01, S_HD2,
-  S_LACC01, S_LACC2, kSlots
+  F_HP = 0, F_HN = 3, F_HV = 6, F_SCOL = 9, F_W = 12, F_PCOL = 13, F_HD = 16, F_LACC = 19, kFields = 22
 };
 
 // LDS ray slots ([field][thread], conflict-free): the only hand-over between
@@ -377,6 +377,14 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
   uint32_t* lvis = ltask + kBlock;                                                             // [kBlock]
   uint32_t* stk = lvis + kBlock + threadIdx.x;
   lvis[threadIdx.x] = 0u;
+  // compaction pool: [0] waves of the block still running and not donors, [1..] per wave the
+  // lanes it handed over (bits cleared as other waves adopt them)
+  uint32_t* pool_live = reinterpret_cast<uint32_t*>(lds_raw + P.pool_off);
+  unsigned long long* pool_mask = reinterpret_cast<unsigned long long*>(lds_raw + P.pool_off + 8);
+  if (threadIdx.x == 0) {
+    *pool_live = kBlock / 64;
+    for (int w = 0; w < kBlock / 64; ++w) pool_mask[w] = 0ull;
+  }
   // once per persistent block: the top treelet and the lights -> LDS
   if (WIDTH == 4 && P.n_top > 0) {
     float4* dst = reinterpret_cast<float4*>(lds_raw + P.top_off);
@@ -394,32 +402,26 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
 
   const int lane = threadIdx.x & 63;
   const unsigned long long lane_below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  // path state, wave-interleaved [wave][slot][64 lanes] x 16 B (see kSlots): buffer ops
-  // with the lane offset in one VGPR and the slot offset s*1024 as an SGPR constant.
+  // path state, wave-interleaved [wave][field][64 lanes] (see kFields): buffer ops with the
+  // lane offset in one VGPR and the field offset f*512 as an SGPR constant.
   const __amdgpu_buffer_rsrc_t prs =
-      __builtin_amdgcn_make_buffer_rsrc(P.pstate, 0, (int)(P.nslots * kSlots * 16), kBufWord3);
-  const uint32_t pvo = ((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * (uint32_t)kSlots * 64u + (uint32_t)lane) * 16u;
-  auto LD2 = [&](int s) { return buf_ld2(prs, pvo, (uint32_t)s * 1024u); };
-  auto ST2 = [&](int s, double a, double b) { buf_st2(prs, pvo, (uint32_t)s * 1024u, a, b); };
-  auto LD1 = [&](int s) { return buf_ld(prs, pvo, (uint32_t)s * 1024u); };
-  auto ST1 = [&](int s, double a) { buf_st(prs, pvo, (uint32_t)s * 1024u, a); };
-  // a vector in slots (s, s+1): x, y in s, z in the first half of s + 1
-  auto LDV = [&](int s) { const D2 q = LD2(s); return d3(q.a, q.b, LD1(s + 1)); };
-  auto STV = [&](int s, D3 v) { ST2(s, v.x, v.y); ST1(s + 1, v.z); };
-  // the shadowable-hit record: HP, HN, HV
-  auto ST_HIT = [&](D3 p, D3 n, D3 v) {
-    ST2(S_HP01, p.x, p.y); ST2(S_HP2_HN0, p.z, n.x); ST2(S_HN12, n.y, n.z); ST2(S_HV01, v.x, v.y); ST1(S_HV2, v.z);
-  };
-  auto LD_HP = [&]() { const D2 a = LD2(S_HP01), b = LD2(S_HP2_HN0); return d3(a.a, a.b, b.a); };
-  auto LD_HN = [&]() { const D2 a = LD2(S_HP2_HN0), b = LD2(S_HN12); return d3(a.b, b.a, b.b); };
-  auto LD_HV = [&]() { return LDV(S_HV01); };
+      __builtin_amdgcn_make_buffer_rsrc(P.pstate, 0, (int)(P.nslots * kFields * sizeof(double)), kBufWord3);
+  // (a lane handed over by tail compaction keeps its pixel's path state: pvo travels with it)
+  uint32_t pvo = ((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * (uint32_t)kFields * 64u + (uint32_t)lane) * 8u;
+  auto LDF = [&](int f) { return buf_ld(prs, pvo, (uint32_t)f * 512u); };
+  auto STF = [&](int f, double v) { buf_st(prs, pvo, (uint32_t)f * 512u, v); };
+  auto LDV = [&](int f) { return d3(LDF(f), LDF(f + 1), LDF(f + 2)); };
+  auto STV = [&](int f, D3 v) { STF(f, v.x); STF(f + 1, v.y); STF(f + 2, v.z); };
+  auto ST_HIT = [&](D3 p, D3 n, D3 v) { STV(F_HP, p); STV(F_HN, n); STV(F_HV, v); };
+  auto LD_HP = [&]() { return LDV(F_HP); };
+  auto LD_HN = [&]() { return LDV(F_HN); };
+  auto LD_HV = [&]() { return LDV(F_HV); };
   // colour and weight carried across mirror bounces
   auto LD_SCOL_W = [&](D3& scol, double& w) {
-    const D2 a = LD2(S_SCOL01), b = LD2(S_SCOL2_W);
-    scol = d3(a.a, a.b, b.a);
-    w = b.b;
+    scol = LDV(F_SCOL);
+    w = LDF(F_W);
   };
-  auto ST_SCOL_W = [&](D3 scol, double w) { ST2(S_SCOL01, scol.x, scol.y); ST2(S_SCOL2_W, scol.z, w); };
+  auto ST_SCOL_W = [&](D3 scol, double w) { STV(F_SCOL, scol); STF(F_W, w); };
 
   // wave-uniform work-head cursor; in list mode the work count comes from the device
   const long long n_list = P.list ? (long long)*P.list_count * P.nsamp : 0;   // work items
@@ -436,7 +438,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
   double thit = DBL_MAX;
   bool shadow_hit = false;
   int batch_end = 0;      // owner: lights [light, batch_end) in flight
-  int refl_h = -1;        // owner: lane tracing its reflection ray this round (-1: none)
+  int refl_h = -1;        // owner: thread tracing its reflection ray this round (-1: none)
   int want = 0;           // owner: extra rays it would lend lanes for
   uint32_t htask = kTaskNone;   // helper: its task word
   unsigned c_primary = 0, c_shadow = 0, c_refl = 0, c_hits = 0;
@@ -540,8 +542,27 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
     if (heads_left == 0 && state == ST_FETCH) state = ST_DONE;
     const bool busy = (state == ST_CLOSEST || state == ST_SHADOW || state >= ST_HSHADOW);
     if (__ballot(busy) == 0) {
-      if (__ballot(state != ST_DONE) == 0) break;
-      continue;
+      if (__ballot(state != ST_DONE) != 0) continue;
+      // every lane done: leave the block's live set.  The last live wave stays while lanes
+      // handed over by donors are still pooled (it adopts them below; no traversal runs).
+      bool leave = true;
+      if (lane == 0) {
+        uint32_t v = *pool_live;
+        for (;;) {
+          if (v >= 2u) {
+            const uint32_t seen = atomicCAS(pool_live, v, v - 1u);
+            if (seen == v) break;
+            v = seen;
+            continue;
+          }
+          bool pooled = false;
+          for (int w = 0; w < kBlock / 64; ++w) pooled |= pool_mask[w] != 0ull;
+          if (pooled) leave = false;
+          else *pool_live = 0u;
+          break;
+        }
+      }
+      if (__shfl(leave ? 1 : 0, 0)) break;
     }
 
     if (STATS) { const unsigned long long t = stamp(); d_fetch += t - t_stamp; t_stamp = t; }
@@ -856,6 +877,9 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
     if (STATS) { const unsigned long long t = stamp(); d_trav += t - t_stamp; t_stamp = t; }
 
     // ---- helpers hand their result to the owner, then go idle ----
+    // (a reflection helper's LDS ray slot still holds the ray its owner reads in SHADE below:
+    // that lane must not adopt a handed-over pixel this iteration)
+    bool refl_held = false;
     {
       const int idle_state = heads_left > 0 ? ST_FETCH : ST_DONE;
       if (state == ST_HSHADOW) {
@@ -865,6 +889,96 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
         ltask[threadIdx.x] = (uint32_t)best;
         *R.tlim = thit;
         state = idle_state;
+        refl_held = true;
+      }
+      wave_lds_sync();
+    }
+
+    // ---- tail compaction: donate (sparse wave, queue empty) or adopt pooled lanes ----
+    if (heads_left == 0) {
+      const int wib = threadIdx.x >> 6;   // wave in block
+      const bool owner = (state == ST_CLOSEST || state == ST_SHADOW);
+      const unsigned long long O = __ballot(owner);
+      if (O != 0ull && __popcll(O) <= kDonateMax && *pool_live >= 2u) {
+        // registers -> this thread's LDS stack entries, then publish the lane mask
+        if (owner) {
+          const unsigned long long tb = (unsigned long long)__double_as_longlong(thit);
+          const uint32_t w[kMigWords] = {
+              (uint32_t)state | (shadow_hit ? 8u : 0u) | ((uint32_t)frame << 4), (uint32_t)px | ((uint32_t)lrow << 16),
+              (uint32_t)py, (uint32_t)sample, (uint32_t)depth, (uint32_t)light, (uint32_t)batch_end, (uint32_t)mesh,
+              (uint32_t)best, (uint32_t)tb, (uint32_t)(tb >> 32), (uint32_t)refl_h, pvo, (uint32_t)item,
+              (uint32_t)((unsigned long long)item >> 32)};
+#pragma unroll
+          for (int k = 0; k < kMigWords; ++k) stk[k * kBlock] = w[k];
+        }
+        wave_lds_sync();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's path-state stores have landed
+        bool donated = false;
+        if (lane == 0) {
+          atomicOr(&pool_mask[wib], O);
+          uint32_t v = *pool_live;   // leave the live set only if another live wave remains
+          while (v >= 2u) {
+            const uint32_t seen = atomicCAS(pool_live, v, v - 1u);
+            if (seen == v) { donated = true; break; }
+            v = seen;
+          }
+        }
+        if (__shfl(donated ? 1 : 0, 0)) break;   // exit: the counters below keep this thread's sums
+        // no other live wave: take back what nobody adopted and carry on
+        unsigned long long back = 0ull;
+        if (lane == 0) back = atomicAnd(&pool_mask[wib], 0ull);
+        back = __shfl(back, 0);
+        if (owner && !((back >> lane) & 1ull)) state = ST_DONE;   // adopted by another wave
+      } else {
+        // adopt pooled lanes of other waves into idle lanes
+        unsigned long long I = __ballot((state == ST_FETCH || state == ST_DONE) && !refl_held);
+        for (int w = 0; w < kBlock / 64 && I != 0ull; ++w) {
+          if (w == wib || pool_mask[w] == 0ull) continue;
+          unsigned long long got = 0ull;
+          if (lane == 0) {
+            unsigned long long m = pool_mask[w], pick = 0ull;
+            for (int k = __popcll(I); k > 0 && m != 0ull; --k) {
+              const unsigned long long b = m & (~m + 1ull);
+              pick |= b;
+              m &= ~b;
+            }
+            got = pick & atomicAnd(&pool_mask[w], ~pick);
+          }
+          got = __shfl(got, 0);
+          const int n = __popcll(got);
+          if (n == 0) continue;
+          // the r-th idle lane takes the r-th adopted lane of donor wave w
+          const bool idle = (I >> lane) & 1ull;
+          const int r = __popcll(I & lane_below);
+          const bool take = idle && r < n;
+          if (take) {
+            const int t = w * 64 + kth_set_bit(got, r);   // donor thread
+            const uint32_t* ds = lvis + kBlock + t;        // its stack entries
+            uint32_t v_[kMigWords];
+#pragma unroll
+            for (int k = 0; k < kMigWords; ++k) v_[k] = ds[k * kBlock];
+            state = (int)(v_[0] & 7u);
+            shadow_hit = (v_[0] & 8u) != 0u;
+            frame = (int)(v_[0] >> 4);
+            px = (int)(v_[1] & 0xffffu);
+            lrow = (int)(v_[1] >> 16);
+            py = (int)v_[2];
+            sample = (int)v_[3];
+            depth = (int)v_[4];
+            light = (int)v_[5];
+            batch_end = (int)v_[6];
+            mesh = (int)v_[7];
+            best = (int)v_[8];
+            thit = __longlong_as_double((long long)(((unsigned long long)v_[10] << 32) | v_[9]));
+            refl_h = (int)v_[11];
+            pvo = v_[12];
+            item = (long long)(((unsigned long long)v_[14] << 32) | v_[13]);
+            lvis[threadIdx.x] = lvis[t];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) lds_d[k * kBlock + threadIdx.x] = lds_d[k * kBlock + t];
+          }
+          I &= ~__ballot(take);
+        }
       }
       wave_lds_sync();
     }
@@ -912,11 +1026,11 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
       if (state == ST_SHADOW) {   // batch finished: lights [light, batch_end) in order
         hp = LD_HP(); hn = LD_HN(); hview = LD_HV();
         const GMat& M = P.mats[mesh];
-        const D3 hdiff = M.tex_w > 0 ? LDV(S_HD01) : d3(M.kd[0], M.kd[1], M.kd[2]);
+        const D3 hdiff = M.tex_w > 0 ? LDV(F_HD) : d3(M.kd[0], M.kd[1], M.kd[2]);
         mirror = M.mirror;
         // first batch: the ambient term (mytracer.cpp:574-576) again, else the stored sum
         D3 lacc = light == 0 ? d3(0.0 + P.amb[0] * M.ka[0], 0.0 + P.amb[1] * M.ka[1], 0.0 + P.amb[2] * M.ka[2])
-                             : LDV(S_LACC01);
+                             : LDV(F_LACC);
         const uint32_t vw = lvis[threadIdx.x];
         for (int j = light; j < batch_end; ++j) {
           const bool occluded = (j == light) ? shadow_hit : (((vw >> (j - light)) & 1u) != 0u);
@@ -926,7 +1040,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
         }
         light = batch_end;
         if (light < P.n_lights) {
-          STV(S_LACC01, lacc);
+          STV(F_LACC, lacc);
           launch_batch(hp, mirror);
         } else {   // bounce complete (subtrace, mytracer.cpp:546-555)
           D3 s0 = d3(0, 0, 0);
@@ -937,7 +1051,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
             ST_SCOL_W(scol, w * mirror);
             depth++;
             if (refl_h >= 0) {   // reflection ray traced by a helper this round
-              const int ht = wbase + refl_h;
+              const int ht = refl_h;
 #pragma unroll
               for (int k = 0; k < 3; ++k) {
                 *R.o[k] = lds_d[k * kBlock + ht];
@@ -1025,7 +1139,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
           light = 0;
           if (M.shadowable && P.n_lights > 0) {   // shadow rays, mytracer.cpp:589-600
             ST_HIT(hp, hn, hview);
-            if (M.tex_w > 0) STV(S_HD01, hdiff);
+            if (M.tex_w > 0) STV(F_HD, hdiff);
             launch_batch(hp, mirror);
           } else {
             for (int j = 0; j < P.n_lights; ++j) lacc = add(lacc, contrib_of(j, hp, hn, hview, hdiff, M));
@@ -1054,10 +1168,10 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
         so[0] = c.x; so[1] = c.y; so[2] = c.z;
         state = heads_left > 0 ? ST_FETCH : ST_DONE;
       } else if (finish) {
-        const D3 pcol = add(sample == 0 ? d3(0, 0, 0) : LDV(S_PCOL01), scol);
+        const D3 pcol = add(sample == 0 ? d3(0, 0, 0) : LDV(F_PCOL), scol);
         sample++;
         if (sample < P.spp_n * P.spp_n) {
-          STV(S_PCOL01, pcol);
+          STV(F_PCOL, pcol);
           start_sample();
         } else {   // compute_image: average, clamp, store (mytracer_gpu.cu:155-159, 221-227)
           const double nn = (double)(P.spp_n * P.spp_n);
@@ -1117,7 +1231,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
               tl = DBL_MAX;
               tw = (uint32_t)lane | kTaskRefl;
               c_refl++;
-              refl_h = ht - wbase;
+              refl_h = ht;
             }
             lds_d[0 * kBlock + ht] = o.x; lds_d[1 * kBlock + ht] = o.y; lds_d[2 * kBlock + ht] = o.z;
             lds_d[3 * kBlock + ht] = d.x; lds_d[4 * kBlock + ht] = d.y; lds_d[5 * kBlock + ht] = d.z;
@@ -1343,12 +1457,13 @@ constexpr int kMaxDepth = 4096;  // traversal stack entries (LDS ring + global s
 // LDS per block: 7 doubles of ray slot, task + visibility words and
 // min(stack_words, kShortStack) stack entries per thread.
 size_t lds_bytes(int stack_words) {
+  stack_words = std::max(stack_words, kMigWords);   // compaction hands registers over in stack entries
   return (size_t)kBlock *
          (7 * sizeof(double) + (2 + (size_t)std::min(stack_words, kShortStack)) * sizeof(uint32_t));
 }
 // ... plus the top treelet (n_top 128-B nodes) after it
 size_t lds_bytes_total(int stack_words, int n_top) {
-  return lds_bytes(stack_words) + (size_t)n_top * sizeof(GNode4) + RT_MAX_LIGHTS * 6 * sizeof(double);
+  return lds_bytes(stack_words) + (size_t)n_top * sizeof(GNode4) + RT_MAX_LIGHTS * 6 * sizeof(double) + kPoolBytes;
 }
 
 }  // namespace
@@ -1362,7 +1477,7 @@ struct LaunchCtx {
   unsigned long long* d_ctr = nullptr;       // [kCtrWords] work heads, stats, diagnostics, then
                                              // FrameDesc[kMaxFrames] (one H2D copy per launch)
   unsigned char* h_ctl = nullptr;            // pinned staging of the same bytes
-  double* d_pstate = nullptr;                // path state, nslots x kSlots x 16 B
+  double* d_pstate = nullptr;                // path state, nslots x kFields fp64
   uint32_t* d_spill = nullptr;               // [stack_words][nslots] (only when stack_words > kShortStack)
   unsigned long long* d_wavelog = nullptr;   // [nslots / 64][4]
   hipEvent_t ev0 = nullptr, ev1 = nullptr;   // kernel start / end (timing, reuse fence)
@@ -2686,7 +2801,7 @@ int upload_image(const SceneImage& I, int device, rt_scene** out) {
   sc->light_cap = RT_MAX_LIGHTS;
   sc->bytes += (long long)(RT_MAX_LIGHTS * 6 * sizeof(double));
   for (LaunchCtx& c : sc->ctx) {
-    const size_t pb = sc->nslots * kSlots * 16;
+    const size_t pb = sc->nslots * kFields * sizeof(double);
     const size_t wb = sc->nslots / 64 * 4 * sizeof(unsigned long long);
     const size_t sb = sc->stack_words > kShortStack ? sc->nslots * (size_t)sc->stack_words * sizeof(uint32_t) : 0;
     if (hipMalloc(reinterpret_cast<void**>(&c.d_ctr), kCtlBytes) != hipSuccess ||
@@ -2786,7 +2901,8 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
     if (std::memcmp(&q, &p[0], sizeof q) != 0)
       return fail(RT_ERR_INVALID, "rt_launch_frames: frames may differ only in camera position and direction");
   }
-  if (p->camera.width <= 0 || p->camera.height <= 0) return fail(RT_ERR_INVALID, "bad image size");
+  if (p->camera.width <= 0 || p->camera.height <= 0 || p->camera.width > 65535 || p->camera.height > 65535)
+    return fail(RT_ERR_INVALID, "bad image size (1..65535 per side)");
   if (p->n_lights < 0 || p->n_lights > (p->lights_ext ? RT_LIGHTS_LIMIT : RT_MAX_LIGHTS))
     return fail(RT_ERR_INVALID, "n_lights out of range (more than RT_MAX_LIGHTS lights need lights_ext)");
   if (p->spp_n < 1 || p->spp_n > 64) return fail(RT_ERR_INVALID, "spp_n must be in [1, 64]");
@@ -2865,6 +2981,7 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   P.n_top = sc->n_top;
   P.top_off = (int)lds_bytes(sc->stack_words);
   P.lights_off = P.top_off + sc->n_top * (int)sizeof(GNode4);
+  P.pool_off = P.lights_off + RT_MAX_LIGHTS * 6 * (int)sizeof(double);
   const long long waves_needed = (P.n_tiles * 64 + 63) / 64;
   int bpc = sc->blocks_per_cu[v];
   if (const char* e = std::getenv("RT_BLOCKS_PER_CU"))   // A/B knob: a smaller persistent grid

@@ -20,8 +20,11 @@ p = hs.render_params(W, H, 1)
 ref, cnt = orc.render(p, pyoracle.MODE_REFERENCE)
 p.out_format = rtamd.RT_OUT_RGB_F64
 img, st = dev.render(p)
-img2, _ = dev.render(p)
+runs = [dev.render(p)[0] for _ in range(4)]
+img2 = runs[0]
 d = np.abs(img - ref).max(-1)
+for r in runs:
+    d = np.maximum(d, np.abs(r - ref).max(-1))
 bad = np.argwhere(d > 1e-12)
 print("counts gpu", st.primary_rays, st.shadow_rays, st.reflection_rays, "oracle", cnt.primary_rays, cnt.shadow_rays,
       cnt.reflection_rays)

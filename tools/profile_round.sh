@@ -11,6 +11,9 @@ export TMPDIR=/tmp
 B="python bench.py --no-cpu-baseline $*"
 timeout -k 10 300 $B > $O/bench_$TAG.json 2> $O/bench_$TAG.err
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$TAG -o run -- $B > $O/prof_$TAG.log 2>&1
+# the traced run prints its own bench line: compare per-shape kernel durations with its HIP events
+grep '^{' $O/prof_$TAG.log | tail -1 > $O/prof_${TAG}_bench.json
+python tools/trace_summary.py $O/trace_$TAG.json $O/prof_$TAG $O/prof_${TAG}_bench.json > /dev/null
 pass() {
   local name=$1; shift
   timeout -k 10 300 rocprofv3 --pmc "$@" --output-format csv -d $O/pmc_${TAG}_$name -o run -- $B > $O/pmc_${TAG}_$name.log 2>&1
