@@ -321,8 +321,10 @@ __device__ __forceinline__ TriOps load_tri(const GTri* tris, uint32_t i) {
 // Path state kept in global memory between a lane's rays, wave-interleaved
 // [wave][field][64 lanes] fp64: one field access of a wave is one b64 buffer instruction over
 // 512 contiguous bytes.  Only what cannot be recomputed is kept:
-//   hit point / normal / view vector of the bounce being shaded (HP, HN, HV: the record of
-//     every shadowable hit, read back when its shadow batch completes);
+//   the normal of the bounce being shaded (HN: the record of every shadowable hit, read back
+//     when its shadow batch completes; the hit point and view vector are recomputed from the
+//     closest-hit ray and its distance, which stay in the owner's LDS ray slot while its own
+//     shadow ray is derived from them at the start of each traversal);
 //   the textured diffuse colour (HD; untextured hits re-read the material's kd);
 //   the light sum across shadow batches (LACC; a bounce whose lights fit one batch restarts
 //     from the recomputed ambient term);
@@ -332,7 +334,7 @@ __device__ __forceinline__ TriOps load_tri(const GTri* tris, uint32_t i) {
 // with b128 accesses were tried: no faster, and some pixels of mirror chains read stale
 // path state under some code layouts -- DESIGN.md §4.)
 enum : int {
-  F_HP = 0, F_HN = 3, F_HV = 6, F_SCOL = 9, F_W = 12, F_PCOL = 13, F_HD = 16, F_LACC = 19, kFields = 22
+  F_HN = 0, F_SCOL = 3, F_W = 6, F_PCOL = 7, F_HD = 10, F_LACC = 13, kFields = 16
 };
 
 // LDS ray slots ([field][thread], conflict-free): the only hand-over between
@@ -412,10 +414,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
   auto STF = [&](int f, double v) { buf_st(prs, pvo, (uint32_t)f * 512u, v); };
   auto LDV = [&](int f) { return d3(LDF(f), LDF(f + 1), LDF(f + 2)); };
   auto STV = [&](int f, D3 v) { STF(f, v.x); STF(f + 1, v.y); STF(f + 2, v.z); };
-  auto ST_HIT = [&](D3 p, D3 n, D3 v) { STV(F_HP, p); STV(F_HN, n); STV(F_HV, v); };
-  auto LD_HP = [&]() { return LDV(F_HP); };
   auto LD_HN = [&]() { return LDV(F_HN); };
-  auto LD_HV = [&]() { return LDV(F_HV); };
   // colour and weight carried across mirror bounces
   auto LD_SCOL_W = [&](D3& scol, double& w) {
     scol = LDV(F_SCOL);
@@ -569,9 +568,20 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
     // ================= TRAVERSE phase =================
     {
       const bool anyhit = (state == ST_SHADOW || state == ST_HSHADOW);
-      const D3 ro = d3(*R.o[0], *R.o[1], *R.o[2]);
-      const D3 rd = d3(*R.d[0], *R.d[1], *R.d[2]);
+      D3 ro = d3(*R.o[0], *R.o[1], *R.o[2]);
+      D3 rd = d3(*R.d[0], *R.d[1], *R.d[2]);
       double tlim = *R.tlim;
+      if (state == ST_SHADOW) {
+        // an owner's own shadow ray for light `light` (mytracer.cpp:589-600), derived from its
+        // closest-hit ray and hit distance kept in the slot: the same operations, in the same
+        // order, as the emission of an explicit ray (emit_ray normalises the direction again)
+        const D3 hp = add(ro, scl(tlim, rd));
+        const D3 to_l = sub(light_of(light).pos, hp);
+        const D3 l = normalize(to_l);
+        ro = add(hp, scl(1e-4, l));
+        rd = normalize(l);
+        tlim = sqrt(dot(to_l, to_l));
+      }
       best = kNoHit;
       best_slot = kNoHit;
       shadow_hit = false;
@@ -975,7 +985,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
             item = (long long)(((unsigned long long)v_[14] << 32) | v_[13]);
             lvis[threadIdx.x] = lvis[t];
 #pragma unroll
-            for (int k = 0; k < 6; ++k) lds_d[k * kBlock + threadIdx.x] = lds_d[k * kBlock + t];
+            for (int k = 0; k < 7; ++k) lds_d[k * kBlock + threadIdx.x] = lds_d[k * kBlock + t];
           }
           I &= ~__ballot(take);
         }
@@ -1010,11 +1020,10 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
                   L6.col.z * (hd_.z * diff + M.ks[2] * refl));
       };
       // own shadow ray for light `light`; the rest of the bounce is offered to idle lanes
-      auto launch_batch = [&](D3 hp_, double mirror_) {
-        const D3 to_l = sub(light_of(light).pos, hp_);
-        const D3 l = normalize(to_l);
+      // (the ray itself is derived at the start of the next traversal from the slot's closest-hit
+      // ray and distance)
+      auto launch_batch = [&](double mirror_) {
         c_shadow++;
-        emit_ray(add(hp_, scl(1e-4, l)), l, sqrt(dot(to_l, to_l)));
         state = ST_SHADOW;
         lvis[threadIdx.x] = 0u;
         batch_end = light + 1;
@@ -1024,7 +1033,13 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
         want = min(rest, kBatchExtra) + ((rest <= kBatchExtra && mirror_ > 0.0 && depth < P.max_depth) ? 1 : 0);
       };
       if (state == ST_SHADOW) {   // batch finished: lights [light, batch_end) in order
-        hp = LD_HP(); hn = LD_HN(); hview = LD_HV();
+        {   // the hit again, from the closest-hit ray and distance kept in the slot
+          const D3 ro = d3(*R.o[0], *R.o[1], *R.o[2]);
+          const D3 rd = d3(*R.d[0], *R.d[1], *R.d[2]);
+          hp = add(ro, scl(*R.tlim, rd));
+          hview = d3(-rd.x, -rd.y, -rd.z);
+        }
+        hn = LD_HN();
         const GMat& M = P.mats[mesh];
         const D3 hdiff = M.tex_w > 0 ? LDV(F_HD) : d3(M.kd[0], M.kd[1], M.kd[2]);
         mirror = M.mirror;
@@ -1041,7 +1056,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
         light = batch_end;
         if (light < P.n_lights) {
           STV(F_LACC, lacc);
-          launch_batch(hp, mirror);
+          launch_batch(mirror);
         } else {   // bounce complete (subtrace, mytracer.cpp:546-555)
           D3 s0 = d3(0, 0, 0);
           double w = 1.0;
@@ -1138,9 +1153,10 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
           D3 lacc = d3(0.0 + P.amb[0] * M.ka[0], 0.0 + P.amb[1] * M.ka[1], 0.0 + P.amb[2] * M.ka[2]);
           light = 0;
           if (M.shadowable && P.n_lights > 0) {   // shadow rays, mytracer.cpp:589-600
-            ST_HIT(hp, hn, hview);
+            STV(F_HN, hn);
+            *R.tlim = thit;   // the slot keeps the closest-hit ray and its distance
             if (M.tex_w > 0) STV(F_HD, hdiff);
-            launch_batch(hp, mirror);
+            launch_batch(mirror);
           } else {
             for (int j = 0; j < P.n_lights; ++j) lacc = add(lacc, contrib_of(j, hp, hn, hview, hdiff, M));
             D3 s0 = d3(0, 0, 0);
