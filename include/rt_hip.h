@@ -98,7 +98,8 @@ enum {
 enum {
   RT_FLAG_TRAVERSAL_STATS = 1, /* canonical counters: 2-wide traversal (the one the oracle replicates),
                                   counts node visits / triangle tests / closest hits */
-  RT_FLAG_WIDE_STATS = 2       /* same counters on the production 4-wide traversal (diagnostics) */
+  RT_FLAG_WIDE_STATS = 2,      /* same counters on the production 4-wide traversal (diagnostics) */
+  RT_FLAG_TIMELINE = 4         /* production kernel + per-round timeline (diagnostics, rt_debug_timeline) */
 };
 
 /* One render call.  Rows are rendered as interleaved stripes:
@@ -257,7 +258,8 @@ int rt_render_to_host(rt_scene* scene, const rt_render_params* p, void* host_out
 int rt_last_kernel_ms(rt_scene* scene, float* ms);
 
 /* Diagnostics: raw device counter words of the last launch (synchronises the
- * device).  Words [8,16) = rt_stats order; with a STATS flag, words [16,30) =
+ * device).  Words [8,16) = rt_stats order (from node_visits on: STATS flags only;
+ * the ray counts [8,11) are the kernel's per-wave slots, summed here); with a STATS flag, words [16,30) =
  * node-loop iterations / active lanes, leaf-loop iterations / active lanes,
  * traverse / shade / refill cycles (s_memtime), outer iterations, traversal
  * rounds / active lanes (per wave, summed), traversal-stack entries spilled
@@ -274,6 +276,16 @@ int rt_debug_counters(rt_scene* scene, unsigned long long* out, int n);
  * fetch, end} (s_memrealtime, 100 MHz) and pixels fetched; waves that were not
  * launched keep stale words.  Synchronises the device; returns words copied. */
 long long rt_debug_wave_log(rt_scene* scene, unsigned long long* out, long long n);
+
+/* Diagnostics: per-round timeline of the last launch with RT_FLAG_TIMELINE: for wave w of the
+ * persistent grid and its r-th traversal round (r < 256), words [8(256w + r), +8) = {round start,
+ * round end} (s_memrealtime, 100 MHz ticks), busy lanes | owner lanes << 8 | (work queue not yet
+ * empty) << 16 | shadow-ray lanes << 24, the most node + leaf iterations of a lane | the wave's
+ * round-loop iterations << 32, then the time (ticks) | count << 40 of the wave-level iterations of
+ * each kind: global-memory node, LDS-treelet node, leaf; last word: the longest wave-level iteration
+ * | the round's setup time << 32.  Unused records are zero.  Synchronises the device; returns
+ * words copied. */
+long long rt_debug_timeline(rt_scene* scene, unsigned long long* out, long long n);
 
 void rt_scene_free(rt_scene* scene);
 

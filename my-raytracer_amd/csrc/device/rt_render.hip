@@ -59,7 +59,7 @@ constexpr int kGroups = 8;          // work heads (XCD groups)
 #define RT_REFILL 16
 #endif
 constexpr int kRefill = RT_REFILL;  // refill a wave when this many lanes are idle
-constexpr int kCtrWords = 40;       // [0,8) work heads, [8,16) stats, [16,40) diagnostics (31: guard)
+constexpr int kCtrWords = 40;       // [8,16) stats (STATS variants), [16,40) diagnostics (31: guard)
 #ifndef RT_SHORT_STACK
 #define RT_SHORT_STACK 16
 #endif
@@ -84,7 +84,8 @@ constexpr int kStackMask = kShortStack - 1;
 #endif
 constexpr int kDonateMax = RT_DONATE_MAX;
 constexpr int kMigWords = 15;
-constexpr int kPoolBytes = 64;   // LDS: live-wave count + one 64-bit lane mask per wave of the block
+constexpr int kPoolBytes = 64;   // LDS: live-wave count, one 64-bit lane mask per wave of the block, exhausted heads
+static_assert(8 + 8 * (RT_BLOCK / 64) + 4 <= kPoolBytes, "compaction pool does not fit");
 static_assert((kShortStack & kStackMask) == 0, "RT_SHORT_STACK must be a power of two");
 
 // Lane states.  Owners carry a pixel (CLOSEST: closest-hit ray in flight; SHADOW: a
@@ -144,6 +145,8 @@ enum : int {
 // the host reports as an error.
 constexpr unsigned kGuardIters = 1u << 24;
 constexpr unsigned kTravGuard = 1u << 24;
+constexpr int kTlCap = 256;   // TL variant: traversal rounds recorded per wave
+constexpr int kTlWords = 8;   // ... and words per round
 
 constexpr int kMaxFrames = RT_MAX_FRAMES;   // frames per launch
 // per-frame camera and output buffer; a launch's table follows its counters in device memory
@@ -153,7 +156,12 @@ struct FrameDesc {
   long long pad;
 };
 static_assert(sizeof(FrameDesc) == 112, "FrameDesc must be 112 bytes");
-constexpr size_t kCtrBytes = kCtrWords * sizeof(unsigned long long);
+// Launch control block (one H2D copy per launch): counter words, the work heads (one per 256-B
+// line: device-scope atomics on one line serialise at the memory side, and a refilling wave
+// waits for its atomic -- DESIGN.md §4 "work heads") and the frame table.
+constexpr size_t kHeadsOff = 512;
+constexpr int kHeadStride = 32;   // u64 words between two work heads
+constexpr size_t kCtrBytes = kHeadsOff + kGroups * 256;
 constexpr size_t kCtlBytes = kCtrBytes + kMaxFrames * sizeof(FrameDesc);
 struct KParams {
   const GNode* nodes;
@@ -167,9 +175,12 @@ struct KParams {
   const unsigned char* texels;
   const GMat* mats;
   unsigned long long* ctr;
+  unsigned long long* heads;  // work head h at heads[h * kHeadStride]
+  unsigned long long* wctr;   // per wave {primary, shadow, reflection, 0} rays (plain stores at exit)
   double* pstate;       // path state, [nslots / 64][kFields][64] fp64
   uint32_t* spill;      // [stack_words][nslots] traversal-stack entries below the LDS ring
   unsigned long long* wavelog;  // STATS: per wave {start, last refill, end, pixels} (s_memrealtime)
+  unsigned long long* tl;       // TL: per wave and traversal round {start, end, lanes, iterations}
   const double* lights; // [n_lights][6] position xyz, colour rgb
   size_t nslots;
   int n_gnodes;
@@ -364,7 +375,7 @@ __device__ __forceinline__ uint32_t u4c(const uint4& v, int c) {
 #define RT_WAVES_PER_EU 4   // 4 waves/SIMD = 16 waves/CU (register budget 128 VGPRs)
 #endif
 
-template <int WIDTH, bool STATS>
+template <int WIDTH, bool STATS, bool TL = false>
 __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render_kernel(KParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   double* lds_d = reinterpret_cast<double*>(lds_raw);
@@ -383,9 +394,12 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
   // lanes it handed over (bits cleared as other waves adopt them)
   uint32_t* pool_live = reinterpret_cast<uint32_t*>(lds_raw + P.pool_off);
   unsigned long long* pool_mask = reinterpret_cast<unsigned long long*>(lds_raw + P.pool_off + 8);
+  // heads this block found exhausted (skipped without an atomic)
+  uint32_t* pool_exh = reinterpret_cast<uint32_t*>(lds_raw + P.pool_off + 8 + 8 * (kBlock / 64));
   if (threadIdx.x == 0) {
     *pool_live = kBlock / 64;
     for (int w = 0; w < kBlock / 64; ++w) pool_mask[w] = 0ull;
+    *pool_exh = 0u;
   }
   // once per persistent block: the top treelet and the lights -> LDS
   if (WIDTH == 4 && P.n_top > 0) {
@@ -447,6 +461,30 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
   unsigned long long d_spills = 0, d_node_lines = 0, d_leaf_lines = 0, d_big_leaf = 0, d_node_lds = 0, d_dummy = 0, d_gn_uni = 0, d_gn_dist = 0, d_leaf_uni = 0;
   unsigned long long w_start = STATS ? __builtin_amdgcn_s_memrealtime() : 0ull, w_refill = 0, w_pixels = 0;
   unsigned long long t_stamp = 0;
+  // TL (round timeline, diagnostics): rounds recorded by this wave, the round's start stamp and
+  // the lane's wave-level node + leaf iterations in it
+  unsigned tl_n = 0;
+  unsigned long long tl_t0 = 0;
+  unsigned tl_it = 0, tl_leaf = 0, tl_spill = 0, tl_gnode = 0;
+  unsigned long long tl_wn = 0, tl_wl = 0, tl_wr = 0, tl_dummy = 0;   // wave-level node / leaf / round iterations
+  // time per wave-level iteration by kind (1 global-memory node, 2 LDS-treelet node, 3 leaf): the
+  // previous iteration's stamp and kind live in ltask[wave's lanes 63, 62] (unused during TRAVERSE);
+  // the first active lane of each iteration charges the time since then to the previous kind
+  unsigned long long tl_gsum[4] = {0, 0, 0, 0}, tl_gcnt[4] = {0, 0, 0, 0}, tl_gap = 0;
+  auto tl_wave_gap = [&](uint32_t kind) {
+    const unsigned long long m = __ballot(1);
+    if (lane == __ffsll((long long)m) - 1) {
+      const uint32_t now = (uint32_t)__builtin_amdgcn_s_memrealtime();
+      const uint32_t prev = ltask[wbase + 63], pk = ltask[wbase + 62];
+      ltask[wbase + 63] = now;
+      ltask[wbase + 62] = kind;
+      const unsigned long long g = now - prev;
+#pragma unroll
+      for (uint32_t k = 0; k < 4; ++k)
+        if (pk == k) { tl_gsum[k] += g; tl_gcnt[k]++; }
+      if (g > tl_gap) tl_gap = g;
+    }
+  };
   auto stamp = [&]() -> unsigned long long { return STATS ? __builtin_amdgcn_s_memtime() : 0ull; };
 
   // light j: position xyz, colour rgb (the branch is wave-uniform)
@@ -497,11 +535,17 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
       const long long g1 = (n_tiles * (head + 1) / kGroups) * 64;
       const int cnt = __popcll(m_fetch);
       const int leader = __ffsll((long long)m_fetch) - 1;
+      if ((*pool_exh >> head) & 1u) {   // another wave of the block found it exhausted
+        head = (head + 1) % kGroups;
+        heads_left--;
+        continue;
+      }
       unsigned long long base = 0;
-      if (lane == leader) base = atomicAdd(&P.ctr[head], (unsigned long long)cnt);
+      if (lane == leader) base = atomicAdd(&P.heads[head * kHeadStride], (unsigned long long)cnt);
       base = __shfl(base, leader);
       const long long start = g0 + (long long)base;
       if (start >= g1) {   // head exhausted: move to the next XCD group's range
+        if (lane == leader) atomicOr(pool_exh, 1u << head);
         head = (head + 1) % kGroups;
         heads_left--;
         continue;
@@ -565,6 +609,16 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
     }
 
     if (STATS) { const unsigned long long t = stamp(); d_fetch += t - t_stamp; t_stamp = t; }
+    if constexpr (TL) {
+      tl_t0 = __builtin_amdgcn_s_memrealtime();
+      tl_it = tl_leaf = tl_spill = tl_gnode = 0;
+      tl_wn = tl_wl = tl_wr = 0;
+      tl_gap = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) tl_gsum[k] = tl_gcnt[k] = 0;
+      if (lane == 0) { ltask[wbase + 63] = (uint32_t)tl_t0; ltask[wbase + 62] = 0u; }
+      wave_lds_sync();
+    }
     // ================= TRAVERSE phase =================
     {
       const bool anyhit = (state == ST_SHADOW || state == ST_HSHADOW);
@@ -656,6 +710,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
           spill[(size_t)slo * P.nslots] = stk[(slo & kStackMask) * kBlock];
           slo++;
           if (STATS) d_spills++;
+          if constexpr (TL) tl_spill++;
         }
         stk[(sp & kStackMask) * kBlock] = x;
         sp++;
@@ -689,6 +744,10 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
           // would run into the end of the record buffer, a fault, not a hang), so it has no watchdog
           for (;;) {
             const uint32_t rec = (WIDTH == 2) ? P.slot2dev[i] : i;
+            if constexpr (TL) {
+              tl_it++; tl_leaf++; wave_tick(tl_wl, tl_dummy, lane);
+              tl_wave_gap(3);
+            }
             if (STATS) {
               c_tris++;
               wave_tick(d_leaf_it, d_leaf_ln, lane);
@@ -755,6 +814,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
           break;
         }
         if (STATS) wave_tick(d_round_it, d_round_ln, lane);
+        if constexpr (TL) wave_tick(tl_wr, tl_dummy, lane);
         if constexpr (WIDTH == 2) {
         for (uint32_t it = 0; !(cur & kLeaf); ++it) {   // internal node (kDone carries the leaf bit)
           if (it > kTravGuard) { guard_trip(); cur = kDone; break; }
@@ -789,6 +849,9 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
         } else {
         for (uint32_t it = 0; !(cur & kLeaf); ++it) {   // 4-wide node: test 4 boxes, visit nearest, push the rest far-first
           if (it > kTravGuard) { guard_trip(); cur = kDone; pleaf = kDone; break; }
+          if constexpr (TL) {
+            tl_it++; wave_tick(tl_wn, tl_dummy, lane);
+          }
           if (STATS) { c_nodes++; wave_tick(d_node_it, d_node_ln, lane); wave_distinct(cur, d_node_lines, lane); }
           float k[4];
           uint32_t v[4];
@@ -798,6 +861,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
           // wave-uniform: every active lane's node is in the LDS treelet -> ds_read, no TD cost
           if (__ballot(cur >= (uint32_t)P.n_top) == 0) {
             if (STATS) wave_tick(d_node_lds, d_dummy, lane);
+            if constexpr (TL) tl_wave_gap(2);
             const unsigned char* lb = lds_raw + P.top_off + cur * (uint32_t)sizeof(GNode4);
             nx = *reinterpret_cast<const float4*>(lb + nxo);
             fx = *reinterpret_cast<const float4*>(lb + (nxo ^ 16u));
@@ -808,6 +872,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
             rf = *reinterpret_cast<const uint4*>(lb + 96);
           } else {
             const char* nb = reinterpret_cast<const char*>(P.nodes4) + (size_t)cur * sizeof(GNode4);
+            if constexpr (TL) { tl_gnode++; tl_wave_gap(1); }
             if (STATS) {
               wave_distinct(cur, d_gn_dist, lane);
               const uint32_t c0 = __shfl(cur, __ffsll((long long)__ballot(1)) - 1);
@@ -887,6 +952,39 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
     }
     asm volatile("" ::: "memory");
     if (STATS) { const unsigned long long t = stamp(); d_trav += t - t_stamp; t_stamp = t; }
+    if constexpr (TL) {   // kTlWords words per round (rt_debug_timeline)
+      tl_wave_gap(0);   // charges the last iteration
+      const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+      unsigned m = tl_it;
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o));
+      const unsigned long long w_r = wave_sum(tl_wr);
+      unsigned long long gs[4], gc[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { gs[k] = wave_sum(tl_gsum[k]); gc[k] = wave_sum(tl_gcnt[k]); }
+      unsigned long long gmax = tl_gap;
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) {
+        const unsigned long long x = __shfl_xor(gmax, o);
+        gmax = x > gmax ? x : gmax;
+      }
+      const unsigned nb = (unsigned)__popcll(__ballot(busy));
+      const unsigned no = (unsigned)__popcll(__ballot(state == ST_CLOSEST || state == ST_SHADOW));
+      const unsigned nsh = (unsigned)__popcll(__ballot(busy && (state == ST_SHADOW || state == ST_HSHADOW)));
+      if (lane == 0 && tl_n < (unsigned)kTlCap) {
+        unsigned long long* r =
+            P.tl + kTlWords * ((size_t)(blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * kTlCap + tl_n);
+        r[0] = tl_t0;
+        r[1] = t1;
+        r[2] = nb | (no << 8) | ((heads_left > 0 ? 1u : 0u) << 16) | ((unsigned long long)nsh << 24);
+        r[3] = m | (w_r << 32);
+        r[4] = gs[1] | (gc[1] << 40);
+        r[5] = gs[2] | (gc[2] << 40);
+        r[6] = gs[3] | (gc[3] << 40);
+        r[7] = gmax | (gs[0] << 32);   // longest iteration; round setup (before the first iteration)
+      }
+      tl_n++;
+    }
 
     // ---- helpers hand their result to the owner, then go idle ----
     // (a reflection helper's LDS ray slot still holds the ray its owner reads in SHADE below:
@@ -1280,9 +1378,9 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
   unsigned long long s3 = 0, s4 = 0, s5 = 0;
   if (STATS) { s3 = wave_sum(c_nodes); s4 = wave_sum(c_tris); s5 = wave_sum(c_hits); }
   if (lane == 0) {
-    atomicAdd(&P.ctr[CS_PRIMARY], s0);
-    atomicAdd(&P.ctr[CS_SHADOW], s1);
-    atomicAdd(&P.ctr[CS_REFLECT], s2);
+    // plain stores to this wave's slot (summed by the host): no contended atomics at exit
+    unsigned long long* wc = P.wctr + 4 * ((size_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6));
+    wc[0] = s0; wc[1] = s1; wc[2] = s2; wc[3] = 0;
     if (STATS) {
       atomicAdd(&P.ctr[CS_NODES], s3);
       atomicAdd(&P.ctr[CS_TRIS], s4);
@@ -1464,13 +1562,15 @@ struct Variant {
 };
 
 // [0] production (4-wide), [1] 4-wide + counters, [2] canonical 2-wide counters
-// (the traversal the oracle replicates: tests pin its node / triangle counts).
+// (the traversal the oracle replicates: tests pin its node / triangle counts),
+// [3] production + per-round timeline (RT_FLAG_TIMELINE, diagnostics).
 const Variant kVariants[] = {
     {render_kernel<4, false>, false},
     {render_kernel<4, true>, true},
     {render_kernel<2, true>, true},
+    {render_kernel<4, false, true>, false},
 };
-constexpr int kNumVariants = 3;
+constexpr int kNumVariants = 4;
 constexpr int kMaxDepth = 4096;  // traversal stack entries (LDS ring + global spill)
 // LDS per block: 7 doubles of ray slot, task + visibility words and
 // min(stack_words, kShortStack) stack entries per thread.
@@ -1498,7 +1598,10 @@ struct LaunchCtx {
   double* d_pstate = nullptr;                // path state, nslots x kFields fp64
   uint32_t* d_spill = nullptr;               // [stack_words][nslots] (only when stack_words > kShortStack)
   unsigned long long* d_wavelog = nullptr;   // [nslots / 64][4]
+  unsigned long long* d_wctr = nullptr;      // [nslots / 64][4] per-wave ray counts
+  unsigned long long* d_tl = nullptr;        // [nslots / 64][kTlCap][kTlWords], allocated by the first TL launch
   hipEvent_t ev0 = nullptr, ev1 = nullptr;   // kernel start / end (timing, reuse fence)
+  long long waves = 0;                       // waves of the last launch (per-wave counter slots)
   bool used = false;
 };
 
@@ -1529,7 +1632,7 @@ struct rt_scene {
   double root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};
   long long bytes = 0;
   int n_cu = 0;
-  int blocks_per_cu[kNumVariants] = {0, 0, 0};
+  int blocks_per_cu[kNumVariants] = {0, 0, 0, 0};
   GNode4* d_nodes4 = nullptr;
   int n_gnodes4 = 0;
   int n_top = 0;                // 4-wide nodes each block caches in LDS
@@ -2387,7 +2490,7 @@ extern "C" {
 const char* rt_last_error(void) { return g_error.c_str(); }
 
 const char* rt_build_info(void) {
-  return "librt_hip: gfx950 persistent flattened render kernel; variants {4-wide, 4-wide+stats, 2-wide canonical stats}; "
+  return "librt_hip: gfx950 persistent flattened render kernel; variants {4-wide, 4-wide+stats, 2-wide canonical stats, 4-wide+round timeline}; "
          "fp32 4-wide nodes (128 B), fp64 triangles/shading, dynamic LDS stack, global path state, 8 XCD work heads";
 }
 
@@ -2826,13 +2929,14 @@ int upload_image(const SceneImage& I, int device, rt_scene** out) {
         hipHostMalloc(reinterpret_cast<void**>(&c.h_ctl), kCtlBytes, hipHostMallocDefault) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&c.d_pstate), pb) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&c.d_wavelog), wb) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&c.d_wctr), wb) != hipSuccess ||
         (sb > 0 && hipMalloc(reinterpret_cast<void**>(&c.d_spill), sb) != hipSuccess) ||
-        hipMemset(c.d_ctr, 0, kCtrWords * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(c.d_ctr, 0, kCtrBytes) != hipSuccess ||
         hipEventCreate(&c.ev0) != hipSuccess || hipEventCreate(&c.ev1) != hipSuccess) {
       rt_scene_free(sc);
       return fail(RT_ERR_HIP, "allocation of launch contexts failed");
     }
-    sc->bytes += (long long)(kCtlBytes + pb + wb + sb);
+    sc->bytes += (long long)(kCtlBytes + pb + 2 * wb + sb);
   }
   *out = sc;
   return RT_OK;
@@ -2899,6 +3003,22 @@ int rt_rows_in_shard(const rt_render_params* p) {
 }  // extern "C"
 
 namespace {
+// Counter words of a finished launch, with the per-wave ray-count slots summed into
+// [CS_PRIMARY, CS_REFLECT] (the kernel stores them per wave instead of adding atomically).
+int read_counters(const LaunchCtx& C, unsigned long long* c) {
+  HIP_TRY(hipMemcpy(c, C.d_ctr, kCtrWords * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  if (C.waves > 0) {
+    std::vector<unsigned long long> w((size_t)C.waves * 4);
+    HIP_TRY(hipMemcpy(w.data(), C.d_wctr, w.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < w.size(); i += 4) {
+      c[CS_PRIMARY] += w[i];
+      c[CS_SHADOW] += w[i + 1];
+      c[CS_REFLECT] += w[i + 2];
+    }
+  }
+  return RT_OK;
+}
+
 // One render launch; list != nullptr: adaptive pass over the pixel ids list[0 .. *count)
 // (at most list_cap of them) of the full frame.
 // n_frames > 1 (rt_launch_frames): params p[0..n_frames) differ only in their camera vectors,
@@ -2942,6 +3062,8 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   LaunchCtx& C = sc->ctx[sc->next_ctx];
   const int ci = sc->next_ctx;
   P.ctr = C.d_ctr;
+  P.heads = reinterpret_cast<unsigned long long*>(reinterpret_cast<unsigned char*>(C.d_ctr) + kHeadsOff);
+  P.wctr = C.d_wctr;
   P.n_frames = n_frames;
   P.frames = reinterpret_cast<const FrameDesc*>(reinterpret_cast<unsigned char*>(C.d_ctr) + kCtrBytes);
   P.n_gnodes = sc->n_gnodes;
@@ -2994,7 +3116,9 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   P.list_count = count;
   P.sample_out = sample_out;
 
-  const int v = (p->flags & RT_FLAG_TRAVERSAL_STATS) ? 2 : ((p->flags & RT_FLAG_WIDE_STATS) ? 1 : 0);
+  const int v = (p->flags & RT_FLAG_TRAVERSAL_STATS) ? 2
+                : (p->flags & RT_FLAG_WIDE_STATS) ? 1
+                : (p->flags & RT_FLAG_TIMELINE) ? 3 : 0;
   const size_t lds = lds_bytes_total(sc->stack_words, sc->n_top);
   P.n_top = sc->n_top;
   P.top_off = (int)lds_bytes(sc->stack_words);
@@ -3024,6 +3148,15 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
     fd[f].out = outs[f];
   }
   HIP_TRY(hipMemcpyAsync(C.d_ctr, C.h_ctl, kCtrBytes + (size_t)n_frames * sizeof(FrameDesc), hipMemcpyHostToDevice, st));
+  if (v == 3) {   // round timeline: zeroed, so unused records read as t = 0
+    const size_t tb = sc->nslots / 64 * kTlCap * kTlWords * sizeof(unsigned long long);
+    if (!C.d_tl) {
+      HIP_TRY(hipMalloc(reinterpret_cast<void**>(&C.d_tl), tb));
+      sc->bytes += (long long)tb;
+    }
+    HIP_TRY(hipMemsetAsync(C.d_tl, 0, tb, st));
+  }
+  P.tl = C.d_tl;
   HIP_TRY(hipEventRecord(C.ev0, st));
   if (rows > 0) {
     void* args[] = {&P};
@@ -3032,12 +3165,14 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   }
   HIP_TRY(hipEventRecord(C.ev1, st));
   C.used = true;
+  C.waves = rows > 0 ? blocks * (kBlock / 64) : 0;
   sc->last_ctx = ci;
   sc->next_ctx = (ci + 1) % kContexts;
   if (stats) {
     HIP_TRY(hipStreamSynchronize(st));
     unsigned long long c[kCtrWords];
-    HIP_TRY(hipMemcpy(c, C.d_ctr, sizeof c, hipMemcpyDeviceToHost));
+    const int rc = read_counters(C, c);
+    if (rc != RT_OK) return rc;
     std::memset(stats, 0, sizeof *stats);
     stats->primary_rays = (long long)c[CS_PRIMARY];
     stats->shadow_rays = (long long)c[CS_SHADOW];
@@ -3185,9 +3320,21 @@ int rt_debug_counters(rt_scene* sc, unsigned long long* out, int n) {
   HIP_TRY(hipDeviceSynchronize());
   unsigned long long c[kCtrWords];
   if (sc->last_ctx < 0) return fail(RT_ERR_INVALID, "rt_debug_counters: no launch recorded");
-  HIP_TRY(hipMemcpy(c, sc->ctx[sc->last_ctx].d_ctr, sizeof c, hipMemcpyDeviceToHost));
+  const int rc = read_counters(sc->ctx[sc->last_ctx], c);
+  if (rc != RT_OK) return rc;
   for (int i = 0; i < n && i < kCtrWords; ++i) out[i] = c[i];
   return std::min(n, kCtrWords);
+}
+
+long long rt_debug_timeline(rt_scene* sc, unsigned long long* out, long long n) {
+  if (!sc || !out || n <= 0) return fail(RT_ERR_INVALID, "rt_debug_timeline: bad argument");
+  HIP_TRY(hipSetDevice(sc->device));
+  HIP_TRY(hipDeviceSynchronize());
+  if (sc->last_ctx < 0 || !sc->ctx[sc->last_ctx].d_tl)
+    return fail(RT_ERR_INVALID, "rt_debug_timeline: the last launch was not an RT_FLAG_TIMELINE launch");
+  const long long words = std::min<long long>(n, (long long)(sc->nslots / 64 * kTlCap * kTlWords));
+  HIP_TRY(hipMemcpy(out, sc->ctx[sc->last_ctx].d_tl, (size_t)words * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  return words;
 }
 
 long long rt_debug_wave_log(rt_scene* sc, unsigned long long* out, long long n) {
@@ -3283,7 +3430,7 @@ void rt_scene_free(rt_scene* sc) {
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   for (LaunchCtx& c : sc->ctx) {
-    void* cp[] = {c.d_ctr, c.d_pstate, c.d_spill, c.d_wavelog};
+    void* cp[] = {c.d_ctr, c.d_pstate, c.d_spill, c.d_wavelog, c.d_tl, c.d_wctr};
     for (void* q : cp)
       if (q) (void)hipFree(q);
     if (c.h_ctl) (void)hipHostFree(c.h_ctl);

@@ -16,7 +16,7 @@ from pathlib import Path
 import numpy as np
 
 from . import abi
-from .abi import RT_OK, RT_OUT_RGB_F32, RT_OUT_RGB_F64, RT_FLAG_TRAVERSAL_STATS, RT_FLAG_WIDE_STATS  # noqa: F401
+from .abi import RT_OK, RT_OUT_RGB_F32, RT_OUT_RGB_F64, RT_FLAG_TRAVERSAL_STATS, RT_FLAG_WIDE_STATS, RT_FLAG_TIMELINE  # noqa: F401
 
 PKG_ROOT = Path(__file__).resolve().parent.parent
 LIB_DIR = PKG_ROOT / "lib"
@@ -336,6 +336,14 @@ class DeviceScene:
         if n < 0:
             _check_hip(int(n), "rt_debug_wave_log")
         return buf[:n].reshape(-1, 4)
+
+    def timeline(self, max_waves=1 << 14):
+        """Per-round records [wave, round, 4] of the last RT_FLAG_TIMELINE launch (rt_debug_timeline)."""
+        buf = np.zeros(8 * 256 * max_waves, dtype=np.uint64)
+        n = hip_lib().rt_debug_timeline(self._h, buf.ctypes.data_as(C.POINTER(C.c_ulonglong)), len(buf))
+        if n < 0:
+            _check_hip(int(n), "rt_debug_timeline")
+        return buf[:n].reshape(-1, 256, 8)
 
     def last_kernel_ms(self):
         ms = C.c_float(0.0)

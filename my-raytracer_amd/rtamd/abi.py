@@ -20,6 +20,7 @@ RT_OUT_RGB_F32 = 0
 RT_OUT_RGB_F64 = 1
 RT_FLAG_TRAVERSAL_STATS = 1
 RT_FLAG_WIDE_STATS = 2
+RT_FLAG_TIMELINE = 4
 
 
 class Material(C.Structure):
@@ -162,6 +163,7 @@ HIP_SYMBOLS = {
     "rt_last_kernel_ms": (C.c_int, [C.c_void_p, C.POINTER(C.c_float)]),
     "rt_debug_counters": (C.c_int, [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]),
     "rt_debug_wave_log": (C.c_longlong, [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_longlong]),
+    "rt_debug_timeline": (C.c_longlong, [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_longlong]),
     "rt_scene_free": (None, [C.c_void_p]),
     "rt_last_error": (C.c_char_p, []),
     "rt_build_info": (C.c_char_p, []),

@@ -1,0 +1,33 @@
+"""One kernel library, office 1080p (dev tool, under gpurun; run by tools/ab_frame.py with
+RTAMD_HIP_LIB set): median kernel time of single-frame launches and of 64-frame launches
+(per frame), printed as one JSON line."""
+import json
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, "my-raytracer_amd")
+import rtamd  # noqa: E402
+
+scene = sys.argv[1] if len(sys.argv) > 1 else "office"
+gen = {"n_triangles": int(sys.argv[2])} if len(sys.argv) > 2 else {}
+host = rtamd.HostScene.generate(scene, **gen)
+host.prepare()
+gpu = rtamd.DeviceScene(host, 0)
+p = host.render_params(1920, 1080, 1)
+out = [torch.zeros((1080, 1920, 3), device="cuda") for _ in range(64)]
+for _ in range(5):
+    gpu.launch(p, out[0].data_ptr())
+single = []
+for _ in range(30):
+    gpu.launch(p, out[0].data_ptr())
+    single.append(gpu.last_kernel_ms())
+cams = [rtamd.camera_orbit(p, 0.12 * (f / 63 - 0.5)) for f in range(64)]
+gpu.launch_frames(cams, [o.data_ptr() for o in out])
+batch = []
+for _ in range(3):
+    gpu.launch_frames(cams, [o.data_ptr() for o in out])
+    batch.append(gpu.last_kernel_ms() / 64)
+print(json.dumps({"single_ms": float(np.median(single)), "single_p90": float(np.percentile(single, 90)),
+                  "batched_ms_per_frame": float(np.median(batch))}), flush=True)
