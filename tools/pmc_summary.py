@@ -4,7 +4,7 @@ usage: python tools/pmc_summary.py OUT.json --bench BENCH.json [--calib CALIB.js
 
 Each DIR holds one pass's *counter_collection.csv over the command that printed
 BENCH.json (the same bench.py command, unprofiled, run just before).  Only the
-production render kernel (render_kernel<4, false>) dispatches count.  Every
+production render kernel (render_kernel<4, false[, false]>) dispatches count.  Every
 counter is summed over those dispatches and divided by the frames they rendered
 (BENCH.json config.production_frames_rendered), so the figures are per frame and
 apply to any launch shape of the same workload (bench.py multiplies by its own
@@ -23,7 +23,9 @@ from collections import defaultdict
 
 
 def is_production(name):
-    return "render_kernel" in name and ("<4, false>" in name or "ILi4ELb0E" in name)
+    # render_kernel<4, false> (round 1) / render_kernel<4, false, false> (mangled ...ILi4ELb0ELb0E...)
+    return "render_kernel" in name and ("<4, false>" in name or "<4, false, false>" in name
+                                        or "ILi4ELb0EEE" in name or "ILi4ELb0ELb0E" in name)
 
 
 def collect(dirs):

@@ -25,10 +25,12 @@ pass ta TA_BUSY_avr
 pass tcc TCC_HIT_sum TCC_MISS_sum
 pass tcp TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum
 pass sq SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SALU
-if [ ! -f $O/hbm_calib.json ]; then
+# FETCH_SIZE/WRITE_SIZE access-width calibration: the committed one (CALIB=...), else measured here
+CAL=${CALIB:-$O/hbm_calib.json}
+if [ ! -f $CAL ]; then
   timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/calib_fetch -o run -- ./tools/hbm_calib.bin > $O/calib_fetch.log 2>&1
   timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/calib_write -o run -- ./tools/hbm_calib.bin > $O/calib_write.log 2>&1
-  python tools/calib_summary.py $O/hbm_calib.json $O/calib_fetch $O/calib_write > /dev/null
+  python tools/calib_summary.py $CAL $O/calib_fetch $O/calib_write > /dev/null
 fi
-python tools/pmc_summary.py $O/pmc_$TAG.json --bench $O/bench_$TAG.json --calib $O/hbm_calib.json $O/pmc_${TAG}_*/
+python tools/pmc_summary.py $O/pmc_$TAG.json --bench $O/bench_$TAG.json --calib $CAL $O/pmc_${TAG}_*/
 echo "profile $TAG done"

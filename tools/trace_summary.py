@@ -25,7 +25,8 @@ def main():
         with open(p) as f:
             for r in csv.DictReader(f):
                 name = r["Kernel_Name"]
-                if "render_kernel<4, false>" in name or "ILi4ELb0E" in name:
+                if any(k in name for k in ("render_kernel<4, false>", "render_kernel<4, false, false>",
+                                           "ILi4ELb0EEE", "ILi4ELb0ELb0E")):
                     rows.append((int(r["Start_Timestamp"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6))
     rows.sort()
     dur = [d for _, d in rows]
