@@ -61,7 +61,7 @@ constexpr int kGroups = 8;          // work heads (XCD groups)
 constexpr int kRefill = RT_REFILL;  // refill a wave when this many lanes are idle
 constexpr int kCtrWords = 40;       // [8,16) stats (STATS variants), [16,40) diagnostics (31: guard)
 #ifndef RT_SHORT_STACK
-#define RT_SHORT_STACK 16
+#define RT_SHORT_STACK 8
 #endif
 // Traversal stack: the top kShortStack entries live in an LDS ring (slot i & kStackMask),
 // deeper entries spill to a per-lane global array.  Bounds LDS per block independently
@@ -70,20 +70,25 @@ constexpr int kShortStack = RT_SHORT_STACK;
 // Top treelet in LDS: the first kTopNodes 4-wide nodes (breadth-first numbering) are copied
 // into each block's LDS; a node iteration whose active lanes all sit in the treelet reads
 // LDS instead of the vector-L1 path.  0 disables.
-#ifndef RT_TOP_NODES
-#define RT_TOP_NODES (RT_BLOCK / 4 - 7)   // fills the CU's 160 KB at 16 waves with the slots, lights and pool
+// LDS per thread: kSlotDoubles fp64 slot words, task + visibility words, the stack ring
+#define RT_SLOT_DOUBLES 10
+#ifndef RT_TOP_NODES   // fills the CU's 160 KB at 4 blocks with the slots, ring, lights, pool
+#define RT_TOP_NODES \
+  ((40960 - RT_BLOCK * (RT_SLOT_DOUBLES * 8 + (2 + RT_SHORT_STACK) * 4) - RT_MAX_LIGHTS * 48 - 64) / 128)
 #endif
 constexpr int kTopNodes = RT_TOP_NODES > 0 ? RT_TOP_NODES : 1;
 constexpr int kStackMask = kShortStack - 1;
 // Tail compaction: once the work queue is empty, a wave with at most kDonateMax
 // pixels in flight hands them to the other waves of its block and exits, so the last pixels
 // of a launch run in fewer, fuller waves.  A handed-over lane's registers travel through the
-// donor thread's LDS stack entries (free between traversals): kMigWords words.
+// donor thread's LDS stack entries (free between traversals): kMigWords words (packed; the
+// closest-hit distance and the hit attributes travel in the LDS slot, copied with it).
 #ifndef RT_DONATE_MAX
 #define RT_DONATE_MAX 24
 #endif
 constexpr int kDonateMax = RT_DONATE_MAX;
-constexpr int kMigWords = 15;
+constexpr int kMigWords = 8;
+static_assert(kMigWords <= kShortStack, "migration words travel in the stack ring entries");
 constexpr int kPoolBytes = 64;   // LDS: live-wave count, one 64-bit lane mask per wave of the block, exhausted heads
 static_assert(8 + 8 * (RT_BLOCK / 64) + 4 <= kPoolBytes, "compaction pool does not fit");
 static_assert((kShortStack & kStackMask) == 0, "RT_SHORT_STACK must be a power of two");
@@ -331,11 +336,8 @@ __device__ __forceinline__ TriOps load_tri(const GTri* tris, uint32_t i) {
 
 // Path state kept in global memory between a lane's rays, wave-interleaved
 // [wave][field][64 lanes] fp64: one field access of a wave is one b64 buffer instruction over
-// 512 contiguous bytes.  Only what cannot be recomputed is kept:
-//   the normal of the bounce being shaded (HN: the record of every shadowable hit, read back
-//     when its shadow batch completes; the hit point and view vector are recomputed from the
-//     closest-hit ray and its distance, which stay in the owner's LDS ray slot while its own
-//     shadow ray is derived from them at the start of each traversal);
+// 512 contiguous bytes.  Only what cannot be recomputed or kept in the LDS slot is kept (the
+// normal of the bounce being shaded lives in the slot's aux words, below):
 //   the textured diffuse colour (HD; untextured hits re-read the material's kd);
 //   the light sum across shadow batches (LACC; a bounce whose lights fit one batch restarts
 //     from the recomputed ambient term);
@@ -345,15 +347,23 @@ __device__ __forceinline__ TriOps load_tri(const GTri* tris, uint32_t i) {
 // with b128 accesses were tried: no faster, and some pixels of mirror chains read stale
 // path state under some code layouts -- DESIGN.md §4.)
 enum : int {
-  F_HN = 0, F_SCOL = 3, F_W = 6, F_PCOL = 7, F_HD = 10, F_LACC = 13, kFields = 16
+  F_SCOL = 0, F_W = 3, F_PCOL = 4, F_HD = 7, F_LACC = 10, kFields = 13
 };
 
-// LDS ray slots ([field][thread], conflict-free): the only hand-over between
-// the shading phase (writes the next ray) and the traversal phase (reads it).
+// LDS slots ([field][thread], conflict-free): the ray (the only hand-over between the
+// shading phase, which writes the next ray, and the traversal phase, which reads it) and
+// three aux words, time-shared:
+//   closest-hit ray in flight: the accepted hit's barycentrics alpha, beta and its mesh id,
+//     written by the leaf test when it accepts a hit, so shading reads them instead of
+//     re-loading the triangle record and recomputing the determinants (same operands, same
+//     operations: bit-identical);
+//   shadow batch in flight: the hit normal HN of the bounce being shaded.
+constexpr int kSlotDoubles = RT_SLOT_DOUBLES;
 struct RaySlots {
   double* o[3];
   double* d[3];
   double* tlim;
+  double* a[3];
 };
 
 // Per-wave loop, two phases:
@@ -386,7 +396,9 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
     R.d[k] = lds_d + (3 + k) * kBlock + threadIdx.x;
   }
   R.tlim = lds_d + 6 * kBlock + threadIdx.x;
-  uint32_t* ltask = reinterpret_cast<uint32_t*>(lds_raw + 7 * kBlock * sizeof(double));   // [kBlock]
+#pragma unroll
+  for (int k = 0; k < 3; ++k) R.a[k] = lds_d + (7 + k) * kBlock + threadIdx.x;
+  uint32_t* ltask = reinterpret_cast<uint32_t*>(lds_raw + kSlotDoubles * kBlock * sizeof(double));   // [kBlock]
   uint32_t* lvis = ltask + kBlock;                                                             // [kBlock]
   uint32_t* stk = lvis + kBlock + threadIdx.x;
   lvis[threadIdx.x] = 0u;
@@ -428,7 +440,8 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
   auto STF = [&](int f, double v) { buf_st(prs, pvo, (uint32_t)f * 512u, v); };
   auto LDV = [&](int f) { return d3(LDF(f), LDF(f + 1), LDF(f + 2)); };
   auto STV = [&](int f, D3 v) { STF(f, v.x); STF(f + 1, v.y); STF(f + 2, v.z); };
-  auto LD_HN = [&]() { return LDV(F_HN); };
+  auto LD_HN = [&]() { return d3(*R.a[0], *R.a[1], *R.a[2]); };
+  auto ST_HN = [&](D3 v) { *R.a[0] = v.x; *R.a[1] = v.y; *R.a[2] = v.z; };
   // colour and weight carried across mirror bounces
   auto LD_SCOL_W = [&](D3& scol, double& w) {
     scol = LDV(F_SCOL);
@@ -792,6 +805,10 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
                       best = (int)rec;
                       best_slot = slot;
                       hi_c = round_up_f(tlim - t_off);
+                      // hit attributes for shading (slot aux words: free while a closest-hit ray is in flight)
+                      *R.a[0] = alpha;
+                      *R.a[1] = beta;
+                      *R.a[2] = __longlong_as_double((long long)T.mesh);
                     }
                   }
                 }
@@ -1012,14 +1029,20 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
       if (O != 0ull && __popcll(O) <= kDonateMax && *pool_live >= 2u) {
         // registers -> this thread's LDS stack entries, then publish the lane mask
         if (owner) {
-          const unsigned long long tb = (unsigned long long)__double_as_longlong(thit);
+          // packed: state (3 bits) | shadow hit | frame (< 128) | sample (< 4096) | refl_h + 1 (9 bits);
+          // item; depth; light; batch size | item >> 32 << 6; best (closest-hit ray) or mesh (shadow
+          // batch); path-state offset; px | lrow << 16.  py is recomputed from lrow; a closest-hit
+          // ray's distance goes to its slot's t-limit word (the slot is copied to the adopter)
+          const unsigned long long it = (unsigned long long)item;
           const uint32_t w[kMigWords] = {
-              (uint32_t)state | (shadow_hit ? 8u : 0u) | ((uint32_t)frame << 4), (uint32_t)px | ((uint32_t)lrow << 16),
-              (uint32_t)py, (uint32_t)sample, (uint32_t)depth, (uint32_t)light, (uint32_t)batch_end, (uint32_t)mesh,
-              (uint32_t)best, (uint32_t)tb, (uint32_t)(tb >> 32), (uint32_t)refl_h, pvo, (uint32_t)item,
-              (uint32_t)((unsigned long long)item >> 32)};
+              (uint32_t)state | (shadow_hit ? 8u : 0u) | ((uint32_t)frame << 4) | ((uint32_t)sample << 11) |
+                  ((uint32_t)(refl_h + 1) << 23),
+              (uint32_t)it, (uint32_t)depth, (uint32_t)light,
+              ((uint32_t)(batch_end - light) & 63u) | ((uint32_t)(it >> 32) << 6),
+              (uint32_t)(state == ST_CLOSEST ? best : mesh), pvo, (uint32_t)px | ((uint32_t)lrow << 16)};
 #pragma unroll
           for (int k = 0; k < kMigWords; ++k) stk[k * kBlock] = w[k];
+          if (state == ST_CLOSEST) *R.tlim = thit;
         }
         wave_lds_sync();
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's path-state stores have landed
@@ -1069,23 +1092,25 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
             for (int k = 0; k < kMigWords; ++k) v_[k] = ds[k * kBlock];
             state = (int)(v_[0] & 7u);
             shadow_hit = (v_[0] & 8u) != 0u;
-            frame = (int)(v_[0] >> 4);
-            px = (int)(v_[1] & 0xffffu);
-            lrow = (int)(v_[1] >> 16);
-            py = (int)v_[2];
-            sample = (int)v_[3];
-            depth = (int)v_[4];
-            light = (int)v_[5];
-            batch_end = (int)v_[6];
-            mesh = (int)v_[7];
-            best = (int)v_[8];
-            thit = __longlong_as_double((long long)(((unsigned long long)v_[10] << 32) | v_[9]));
-            refl_h = (int)v_[11];
-            pvo = v_[12];
-            item = (long long)(((unsigned long long)v_[14] << 32) | v_[13]);
+            frame = (int)((v_[0] >> 4) & 127u);
+            sample = (int)((v_[0] >> 11) & 4095u);
+            refl_h = (int)(v_[0] >> 23) - 1;
+            item = (long long)(((unsigned long long)(v_[4] >> 6) << 32) | v_[1]);
+            depth = (int)v_[2];
+            light = (int)v_[3];
+            batch_end = light + (int)(v_[4] & 63u);
+            if (state == ST_CLOSEST) best = (int)v_[5];
+            else mesh = (int)v_[5];
+            pvo = v_[6];
+            px = (int)(v_[7] & 0xffffu);
+            lrow = (int)(v_[7] >> 16);
+            py = (P.stripe_count == 1)
+                     ? P.row_begin + lrow
+                     : ((lrow / P.stripe_h) * P.stripe_count + P.stripe_index) * P.stripe_h + (lrow % P.stripe_h);
             lvis[threadIdx.x] = lvis[t];
 #pragma unroll
-            for (int k = 0; k < 7; ++k) lds_d[k * kBlock + threadIdx.x] = lds_d[k * kBlock + t];
+            for (int k = 0; k < kSlotDoubles; ++k) lds_d[k * kBlock + threadIdx.x] = lds_d[k * kBlock + t];
+            thit = *R.tlim;   // a closest-hit ray's distance (a shadow batch's owner does not read thit)
           }
           I &= ~__ballot(take);
         }
@@ -1174,6 +1199,8 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
               }
               best = (int)ltask[ht];
               thit = lds_d[6 * kBlock + ht];
+#pragma unroll
+              for (int k = 0; k < 3; ++k) *R.a[k] = lds_d[(7 + k) * kBlock + ht];   // its hit attributes
               hit_ready = true;
             } else {
               const D3 d = d3(-hview.x, -hview.y, -hview.z);   // reflect(d, n) = d - 2(n.d)n
@@ -1213,21 +1240,20 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
             const GMat& Mp = P.mats[mesh];
             hdiff = d3(Mp.kd[0], Mp.kd[1], Mp.kd[2]);
           } else {
-            // the normal record is indexed by the hit record: its loads issue together with the
-            // triangle's (one dependent level fewer than face / vertex-id -> vertex-normal gathers)
-            const double2* nq = reinterpret_cast<const double2*>(P.tnorm + 12 * (size_t)best);
-            const double2 q0 = nq[0], q1 = nq[1], q2 = nq[2], q3 = nq[3], q4 = nq[4], q5 = nq[5];
-            const TriOps T = load_tri(P.tris, (uint32_t)best);
-            const D3 c4 = sub(ro, T.p2);
-            const double S = det3(T.e1, T.e2, c3);
-            const double alpha = det3(c4, T.e2, c3) / S;
-            const double beta = det3(T.e1, c4, c3) / S;
+            // barycentrics and mesh from the leaf test that accepted the hit (slot aux words: the
+            // CPU's Da / S and Db / S of mymesh.cpp:205-215 on the same operands); the normal
+            // record is indexed by the hit record
+            const double alpha = *R.a[0], beta = *R.a[1];
             const double gamma = (1.0 - alpha - beta);
-            mesh = T.mesh;
+            mesh = (int)__double_as_longlong(*R.a[2]);
             const GMat& Mt = P.mats[mesh];
+            const double* nr = P.tnorm + 12 * (size_t)best;
             if (Mt.draw_mode == RT_DRAW_FLAT) {   // normals_[i] (mytracer_gpu.cu:498-500)
-              hn = d3(q0.x, q0.y, q1.x);
+              const double2 q0 = *reinterpret_cast<const double2*>(nr);
+              hn = d3(q0.x, q0.y, nr[2]);
             } else {   // alpha*vn0 + beta*vn1 + gamma*vn2, not renormalised (:501-505)
+              const double2* nq = reinterpret_cast<const double2*>(nr + 2);   // [2, 12): _, vn0, vn1, vn2
+              const double2 q1 = nq[0], q2 = nq[1], q3 = nq[2], q4 = nq[3], q5 = nq[4];
               const double n0[3] = {q1.y, q2.x, q2.y}, n1[3] = {q3.x, q3.y, q4.x}, n2[3] = {q4.y, q5.x, q5.y};
               hn = d3(alpha * n0[0] + beta * n1[0] + gamma * n2[0], alpha * n0[1] + beta * n1[1] + gamma * n2[1],
                       alpha * n0[2] + beta * n1[2] + gamma * n2[2]);
@@ -1253,7 +1279,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
           D3 lacc = d3(0.0 + P.amb[0] * M.ka[0], 0.0 + P.amb[1] * M.ka[1], 0.0 + P.amb[2] * M.ka[2]);
           light = 0;
           if (M.shadowable && P.n_lights > 0) {   // shadow rays, mytracer.cpp:589-600
-            STV(F_HN, hn);
+            ST_HN(hn);
             *R.tlim = thit;   // the slot keeps the closest-hit ray and its distance
             if (M.tex_w > 0) STV(F_HD, hdiff);
             launch_batch(mirror);
@@ -1572,12 +1598,12 @@ const Variant kVariants[] = {
 };
 constexpr int kNumVariants = 4;
 constexpr int kMaxDepth = 4096;  // traversal stack entries (LDS ring + global spill)
-// LDS per block: 7 doubles of ray slot, task + visibility words and
+// LDS per block: kSlotDoubles doubles of slot, task + visibility words and
 // min(stack_words, kShortStack) stack entries per thread.
 size_t lds_bytes(int stack_words) {
   stack_words = std::max(stack_words, kMigWords);   // compaction hands registers over in stack entries
   return (size_t)kBlock *
-         (7 * sizeof(double) + (2 + (size_t)std::min(stack_words, kShortStack)) * sizeof(uint32_t));
+         (kSlotDoubles * sizeof(double) + (2 + (size_t)std::min(stack_words, kShortStack)) * sizeof(uint32_t));
 }
 // ... plus the top treelet (n_top 128-B nodes) after it
 size_t lds_bytes_total(int stack_words, int n_top) {
