@@ -240,18 +240,27 @@ def test_full_size_office_1080p_parity():
     assert counts(st) == [cnt.primary_rays, cnt.shadow_rays, cnt.reflection_rays]
 
 
-def test_full_size_4k_16spp_sampled_rows():
-    # BASELINE config 3 (3840x2160, 4x4 stratified): sampled rows vs the oracle,
-    # exact primary count for the whole frame.
+def test_full_size_4k_16spp_every_8th_row():
+    # BASELINE config 3 (3840x2160, 4x4 stratified): every 8th row (1.04 M pixels, 16.6 M
+    # samples) against the oracle, with the exact ray counts of those rows (rendered again as
+    # the 1-row stripe shard 3 of 8), and the exact primary count of the whole frame.
     hs, dev, orc = Case.get("office")
     p = hs.render_params(3840, 2160, 4)
     p.out_format = rtamd.RT_OUT_RGB_F64
     img, st = dev.render(p)
     assert st.primary_rays == 3840 * 2160 * 16
-    ys = np.arange(3, 2160, 97)
-    xy = np.stack(np.meshgrid(np.arange(3840), ys), -1).reshape(-1, 2)
-    ref, _ = orc.render_pixels(p, xy, pyoracle.MODE_REFERENCE)
+    ys = np.arange(3, 2160, 8)
+    xy = np.stack(np.meshgrid(np.arange(3840), ys), -1).reshape(-1, 2).astype(np.int32)
+    ref, cnt = orc.render_pixels(p, xy, pyoracle.MODE_ORDERED, threads=0)
     assert np.abs(img[ys].reshape(-1, 3) - ref).max() <= TOL64
+    rng = np.random.default_rng(7)   # and reference-semantics traversal on 3000 random pixels
+    xr = np.stack([rng.integers(0, 3840, 3000), rng.integers(0, 2160, 3000)], 1).astype(np.int32)
+    ref2, _ = orc.render_pixels(p, xr, pyoracle.MODE_REFERENCE, threads=0)
+    assert np.abs(img[xr[:, 1], xr[:, 0]] - ref2).max() <= TOL64
+    p.stripe_height, p.stripe_count, p.stripe_index = 1, 8, 3
+    img8, st8 = dev.render(p)
+    assert np.array_equal(img8, img[ys])
+    assert counts(st8) == [cnt.primary_rays, cnt.shadow_rays, cnt.reflection_rays]
 
 
 def test_config4_10m_random_triangles_full_frame():
@@ -286,9 +295,10 @@ def test_config4_10m_random_triangles_full_frame():
     assert dev.debug_counters()["stack_spills"] > 0
 
 
-def test_config5_8k_64spp_one_of_8_shards_sampled_pixels():
+def test_config5_8k_64spp_one_of_8_shards_every_12th_row():
     # BASELINE config 5 (7680x4320, 8x8 stratified, rows sharded over 8 GPUs): the shard of
-    # rank 3 renders on this GPU; sampled pixels against the oracle at their global rows.
+    # rank 3 renders on this GPU; every 12th of its rows (45 rows, 22 M samples) against the
+    # oracle at their global rows, plus 150 random pixels of the shard.
     hs, dev, orc = Case.get("office")
     p = hs.render_params(7680, 4320, 8)
     p.stripe_height, p.stripe_count, p.stripe_index = 16, 8, 3
@@ -296,10 +306,14 @@ def test_config5_8k_64spp_one_of_8_shards_sampled_pixels():
     img, st = dev.render(p)
     rows = rtamd.shard_rows(4320, 16, 8, 3)
     assert img.shape == (len(rows), 7680, 3) and st.primary_rays == len(rows) * 7680 * 64
+    q = hs.render_params(7680, 4320, 8)
+    li = np.arange(5, len(rows), 12)
+    xy = np.stack(np.meshgrid(np.arange(7680), rows[li]), -1).reshape(-1, 2).astype(np.int32)
+    ref, _ = orc.render_pixels(q, xy, pyoracle.MODE_ORDERED, threads=0)
+    assert np.abs(img[li].reshape(-1, 3) - ref).max() <= TOL64
     rng = np.random.default_rng(11)
     li = rng.integers(0, len(rows), 150)
     xs = rng.integers(0, 7680, 150)
-    q = hs.render_params(7680, 4320, 8)
     ref, _ = orc.render_pixels(q, np.stack([xs, rows[li]], 1).astype(np.int32), pyoracle.MODE_REFERENCE)
     assert np.abs(img[li, xs] - ref).max() <= TOL64
 
