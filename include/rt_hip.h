@@ -277,6 +277,10 @@ int rt_debug_counters(rt_scene* scene, unsigned long long* out, int n);
  * launched keep stale words.  Synchronises the device; returns words copied. */
 long long rt_debug_wave_log(rt_scene* scene, unsigned long long* out, long long n);
 
+/* Diagnostics: persistent-grid blocks per CU of kernel variant 0 (production), 1 (4-wide
+ * STATS), 2 (2-wide canonical STATS) or 3 (timeline), as the launches use it. */
+int rt_debug_blocks_per_cu(rt_scene* scene, int variant);
+
 /* Diagnostics: per-round timeline of the last launch with RT_FLAG_TIMELINE: for wave w of the
  * persistent grid and its r-th traversal round (r < 256), words [8(256w + r), +8) = {round start,
  * round end} (s_memrealtime, 100 MHz ticks), busy lanes | owner lanes << 8 | (work queue not yet

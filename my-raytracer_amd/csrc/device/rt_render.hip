@@ -2937,6 +2937,15 @@ int upload_image(const SceneImage& I, int device, rt_scene** out) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(kVariants[v].fn), kBlock, lds) !=
             hipSuccess || nb < 1)
       nb = 1;
+    // the occupancy API can report one block per CU more than fits (MI355X_MICROARCH.md: at some
+    // SGPR counts), which would leave a persistent grid's last blocks waiting for the first to
+    // exit: bound it by the VGPR file (512 per SIMD lane, granule 8) and the CU's 160 KB of LDS
+    hipFuncAttributes fa;
+    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(kVariants[v].fn)) == hipSuccess && fa.numRegs > 0) {
+      const int waves_per_simd = 512 / ((fa.numRegs + 7) / 8 * 8);
+      nb = std::min(nb, std::max(1, waves_per_simd * 4 / (kBlock / 64)));
+    }
+    nb = std::min(nb, std::max(1, (int)(160 * 1024 / lds)));
     sc->blocks_per_cu[v] = nb;
     max_blocks = std::max(max_blocks, nb);
   }
@@ -3350,6 +3359,11 @@ int rt_debug_counters(rt_scene* sc, unsigned long long* out, int n) {
   if (rc != RT_OK) return rc;
   for (int i = 0; i < n && i < kCtrWords; ++i) out[i] = c[i];
   return std::min(n, kCtrWords);
+}
+
+int rt_debug_blocks_per_cu(rt_scene* sc, int variant) {
+  if (!sc || variant < 0 || variant >= kNumVariants) return fail(RT_ERR_INVALID, "rt_debug_blocks_per_cu: bad argument");
+  return sc->blocks_per_cu[variant];
 }
 
 long long rt_debug_timeline(rt_scene* sc, unsigned long long* out, long long n) {

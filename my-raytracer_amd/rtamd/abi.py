@@ -164,6 +164,7 @@ HIP_SYMBOLS = {
     "rt_debug_counters": (C.c_int, [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]),
     "rt_debug_wave_log": (C.c_longlong, [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_longlong]),
     "rt_debug_timeline": (C.c_longlong, [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_longlong]),
+    "rt_debug_blocks_per_cu": (C.c_int, [C.c_void_p, C.c_int]),
     "rt_scene_free": (None, [C.c_void_p]),
     "rt_last_error": (C.c_char_p, []),
     "rt_build_info": (C.c_char_p, []),
