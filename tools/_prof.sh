@@ -1,4 +1,4 @@
 set -e -o pipefail
 export CALIB=profiles/r02/hbm_calib.json
-bash tools/profile_round.sh r02q
-bash tools/profile_round.sh r02q_rt10m --scene random_tris --tris 10000000 --steps 64 --warmup 32 --single-frames 4
+bash tools/profile_round.sh r02r
+timeout -k 10 300 python bench.py > gpurun_out/bench_r02r_full.json 2> gpurun_out/bench_r02r_full.err
