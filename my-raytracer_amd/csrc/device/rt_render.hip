@@ -502,8 +502,16 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
 
   // light j: position xyz, colour rgb (the branch is wave-uniform)
   struct Light6 { D3 pos, col; };
+  // (two explicitly typed paths: a pointer chosen between LDS and global memory would make every
+  // light read a flat load through the vector-memory pipeline)
+  typedef __attribute__((address_space(3))) double lds_double;
+  typedef __attribute__((address_space(1))) const double glb_double;
   auto light_of = [&](int j) -> Light6 {
-    const double* L = lights_lds ? lds_lights + 6 * j : P.lights + 6 * (size_t)j;
+    if (lights_lds) {
+      const lds_double* L = (const lds_double*)(lds_double*)(lds_lights) + 6 * j;
+      return Light6{d3(L[0], L[1], L[2]), d3(L[3], L[4], L[5])};
+    }
+    const glb_double* L = (const glb_double*)(P.lights) + 6 * (size_t)j;
     return Light6{d3(L[0], L[1], L[2]), d3(L[3], L[4], L[5])};
   };
 
