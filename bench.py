@@ -8,8 +8,9 @@ One step = one full frame: every rank renders its interleaved 16-row stripes
 (stripe = rank mod N) with one launch of the flattened HIP kernel, then rank 0
 gathers the stripes over RCCL (torch.distributed "nccl") and re-interleaves
 them into the final image.  Total work per step is fixed => "strong" scaling.
-Consecutive frames are rendered --frames at a time (default 128, at most --steps)
-by ONE launch of the persistent kernel (rt_launch_frames: the frames share one
+Consecutive frames are rendered --frames at a time (default 128, at most --steps; at N > 1
+at most half of --steps, so the timed run has two launches or more and each gather overlaps the
+next launch) by ONE launch of the persistent kernel (rt_launch_frames: the frames share one
 work queue, so the drain at the end of a launch is paid once per F frames).  The
 F frames of a launch follow an animation path (rtamd.camera_orbit, --sweep): they
 are distinct views, and every frame traces all of its rays.  A single_frame record
@@ -147,6 +148,10 @@ def main():
     frame_bytes = rows_max * W * 3 * 4
     F = 1 if a.adaptive else max(1, min(a.frames or 128, rtamd.abi.RT_MAX_FRAMES, a.steps,
                                         int(a.frame_budget_gb * 1e9 // frame_bytes)))
+    if n > 1 and not a.frames and not a.adaptive:
+        # N > 1: at least two launches in the timed run, so the gather of one launch overlaps the
+        # rendering of the next (a single launch would leave its whole gather exposed)
+        F = min(F, max(1, (a.steps + 1) // 2))
     # the animation path: frame f of every launch (the batched frames are distinct views)
     if F > 1 and a.sweep != 0.0:
         cams = [rtamd.camera_orbit(params, a.sweep * (f / (F - 1) - 0.5)) for f in range(F)]
