@@ -99,8 +99,11 @@ static_assert((kShortStack & kStackMask) == 0, "RT_SHORT_STACK must be a power o
 // extra shadow rays or its reflection ray, so a bounce costs one round, not 1 + lights.
 enum : int { ST_FETCH = 0, ST_CLOSEST = 1, ST_SHADOW = 2, ST_DONE = 3, ST_HSHADOW = 4, ST_HCLOSEST = 5 };
 constexpr uint32_t kTaskNone = 0xffffffffu;
-// task word: owner lane | (light - owner's first light of the batch) << 8, or owner lane | kTaskRefl
-constexpr uint32_t kTaskRefl = 0x10000u;
+// task word: owner lane | (light - owner's first light of the batch) << 6 | light << 11, or
+// owner lane | kTaskRefl.  The helper derives its ray itself at the start of the traversal from
+// the owner's slot (closest-hit ray, hit distance, hit normal in the aux words).
+constexpr uint32_t kTaskRefl = 0x80000000u;
+static_assert(RT_LIGHTS_LIMIT <= (1 << 20), "light index must fit the task word");
 // a bounce's shadow rays go out in batches of at most 1 + kBatchExtra lights (the owner's
 // own ray + one helper per extra light): the helpers' occlusion bits fit one LDS word
 constexpr int kBatchExtra = 31;
@@ -643,19 +646,34 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
     // ================= TRAVERSE phase =================
     {
       const bool anyhit = (state == ST_SHADOW || state == ST_HSHADOW);
-      D3 ro = d3(*R.o[0], *R.o[1], *R.o[2]);
-      D3 rd = d3(*R.d[0], *R.d[1], *R.d[2]);
-      double tlim = *R.tlim;
-      if (state == ST_SHADOW) {
-        // an owner's own shadow ray for light `light` (mytracer.cpp:589-600), derived from its
-        // closest-hit ray and hit distance kept in the slot: the same operations, in the same
-        // order, as the emission of an explicit ray (emit_ray normalises the direction again)
+      // helpers read their owner's slot (its closest-hit ray and hit distance)
+      const int src = (state >= ST_HSHADOW) ? wbase + (int)(htask & 63u) : (int)threadIdx.x;
+      D3 ro = d3(lds_d[0 * kBlock + src], lds_d[1 * kBlock + src], lds_d[2 * kBlock + src]);
+      D3 rd = d3(lds_d[3 * kBlock + src], lds_d[4 * kBlock + src], lds_d[5 * kBlock + src]);
+      double tlim = lds_d[6 * kBlock + src];
+      if (anyhit) {
+        // a shadow ray (mytracer.cpp:589-600) for light j of the owner's bounce, derived from the
+        // closest-hit ray and hit distance kept in the owner's slot: the same operations, in the
+        // same order, as the emission of an explicit ray (emit_ray normalises the direction again)
+        const int j = (state == ST_SHADOW) ? light : (int)((htask >> 11) & 0xFFFFFu);
         const D3 hp = add(ro, scl(tlim, rd));
-        const D3 to_l = sub(light_of(light).pos, hp);
+        const D3 to_l = sub(light_of(j).pos, hp);
         const D3 l = normalize(to_l);
         ro = add(hp, scl(1e-4, l));
         rd = normalize(l);
         tlim = sqrt(dot(to_l, to_l));
+      } else if (state == ST_HCLOSEST) {
+        // the owner's reflection ray (mytracer.cpp:547-552), from its hit and its normal (the
+        // owner's aux words); kept in this helper's slot, from which the owner takes it over
+        const D3 hp = add(ro, scl(tlim, rd));
+        const D3 hn = d3(lds_d[7 * kBlock + src], lds_d[8 * kBlock + src], lds_d[9 * kBlock + src]);
+        const double s2 = 2.0 * dot(hn, rd);   // reflect(d, n) = d - 2(n.d)n, d = -view = rd
+        const D3 v = sub(rd, scl(s2, hn));
+        ro = add(hp, scl(1e-4, v));
+        rd = normalize(v);
+        tlim = DBL_MAX;
+        *R.o[0] = ro.x; *R.o[1] = ro.y; *R.o[2] = ro.z;
+        *R.d[0] = rd.x; *R.d[1] = rd.y; *R.d[2] = rd.z;
       }
       best = kNoHit;
       best_slot = kNoHit;
@@ -1018,7 +1036,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
     {
       const int idle_state = heads_left > 0 ? ST_FETCH : ST_DONE;
       if (state == ST_HSHADOW) {
-        if (shadow_hit) atomicOr(&lvis[wbase + (int)(htask & 63u)], 1u << ((htask >> 8) & 31u));   // bit: light - batch start
+        if (shadow_hit) atomicOr(&lvis[wbase + (int)(htask & 63u)], 1u << ((htask >> 6) & 31u));   // bit: light - batch start
         state = idle_state;
       } else if (state == ST_HCLOSEST) {
         ltask[threadIdx.x] = (uint32_t)best;
@@ -1128,11 +1146,8 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
 
     // ================= SHADE phase (owners) =================
     want = 0;
-    // the hit being shaded: live from SHADE into the fan-out below (an owner that offers rays
-    // has just computed or loaded them), so the fan-out never reads back path state the wave
-    // stored in this same iteration
-    D3 hp = d3(0, 0, 0), hn = d3(0, 0, 0), hview = d3(0, 0, 0);
     if (state == ST_CLOSEST || state == ST_SHADOW) {
+      D3 hp = d3(0, 0, 0), hn = d3(0, 0, 0), hview = d3(0, 0, 0);   // the hit being shaded
       bool hit_ready = (state == ST_CLOSEST), finish = false;
       D3 scol = d3(0, 0, 0);   // the sample's colour so far once the path ends (finish)
       double mirror = 0.0;
@@ -1358,34 +1373,17 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
         const int got = min(want, max(0, avail - off));
         if (got > 0) {
           const int n_extra_lights = min(P.n_lights - light - 1, kBatchExtra);
-          for (int t = 0; t < got; ++t) {
+          for (int t = 0; t < got; ++t) {   // task words only: each helper derives its own ray
             const int ht = wbase + kth_set_bit(I, off + t);
-            D3 o, d;
-            double tl;
             uint32_t tw;
             if (t < n_extra_lights) {
-              const int j = light + 1 + t;
-              const D3 to_l = sub(light_of(j).pos, hp);
-              const D3 l = normalize(to_l);
-              o = add(hp, scl(1e-4, l));
-              d = normalize(l);
-              tl = sqrt(dot(to_l, to_l));
-              tw = (uint32_t)lane | ((uint32_t)(t + 1) << 8);
+              tw = (uint32_t)lane | ((uint32_t)(t + 1) << 6) | ((uint32_t)(light + 1 + t) << 11);
               c_shadow++;
-            } else {   // reflection ray (same formula as the owner's own emission)
-              const D3 dd = d3(-hview.x, -hview.y, -hview.z);
-              const double s2 = 2.0 * dot(hn, dd);
-              const D3 v = sub(dd, scl(s2, hn));
-              o = add(hp, scl(1e-4, v));
-              d = normalize(v);
-              tl = DBL_MAX;
+            } else {   // reflection ray
               tw = (uint32_t)lane | kTaskRefl;
               c_refl++;
               refl_h = ht;
             }
-            lds_d[0 * kBlock + ht] = o.x; lds_d[1 * kBlock + ht] = o.y; lds_d[2 * kBlock + ht] = o.z;
-            lds_d[3 * kBlock + ht] = d.x; lds_d[4 * kBlock + ht] = d.y; lds_d[5 * kBlock + ht] = d.z;
-            lds_d[6 * kBlock + ht] = tl;
             ltask[ht] = tw;
           }
           batch_end = light + 1 + min(got, n_extra_lights);
