@@ -206,6 +206,8 @@ MULTI_SYMBOLS = {
 
 def bind(lib, table):
     for name, (res, args) in table.items():
+        if name.startswith("rt_debug_") and not hasattr(lib, name):
+            continue   # diagnostics a kernel variant library built from an older source lacks (A/B tools)
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
