@@ -107,7 +107,7 @@ def parse():
 def workload_key(a, n):
     """Identity of the profiled workload: the PMC summary of a run applies to runs with the same key."""
     return {"scene": a.scene, "tris": a.tris, "width": a.width, "height": a.height, "spp": a.spp, "tree": a.tree,
-            "sweep": a.sweep if not a.adaptive else 0.0, "adaptive": bool(a.adaptive),
+            "sweep": a.sweep if (not a.adaptive or n == 1) else 0.0, "adaptive": bool(a.adaptive),
             "analytic": bool(a.analytic or a.scene == "spheres"), "n_gpus": n}
 
 
@@ -145,9 +145,13 @@ def main():
     rows_max = shard_max_rows(a.height, STRIPE_H, n)
     # librt_hip keeps 8 launch contexts per scene; the halo exchange of --adaptive is single-stream
     S = 1 if a.adaptive else max(1, min(a.streams or (1 if n == 1 else 2), 8))
-    frame_bytes = rows_max * W * 3 * 4
-    F = 1 if a.adaptive else max(1, min(a.frames or 128, rtamd.abi.RT_MAX_FRAMES, a.steps,
-                                        int(a.frame_budget_gb * 1e9 // frame_bytes)))
+    # --adaptive on one GPU: F frames per launch for both passes (rt_launch_frames for the fp64
+    # primary images, rt_launch_adaptive_frames for the supersampling of all F frames); on N > 1
+    # one frame per launch (the halo exchange is per frame)
+    batched_adaptive = a.adaptive and n == 1
+    frame_bytes = rows_max * W * 3 * (4 + (8 if a.adaptive else 0))
+    F = 1 if (a.adaptive and not batched_adaptive) else max(1, min(a.frames or 128, rtamd.abi.RT_MAX_FRAMES, a.steps,
+                                                                   int(a.frame_budget_gb * 1e9 // frame_bytes)))
     if n > 1 and not a.frames and not a.adaptive:
         # N > 1: at least two launches in the timed run, so the gather of one launch overlaps the
         # rendering of the next (a single launch would leave its whole gather exposed)
@@ -163,8 +167,13 @@ def main():
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(S - 1)]
     stream = streams[0].cuda_stream
     rows_local = rtamd.rows_in_shard(params)
-    prims = [torch.zeros((rows_max, W, 3), dtype=torch.float64, device="cuda")
+    prims = [torch.zeros((F, rows_max, W, 3), dtype=torch.float64, device="cuda")
              for _ in range(S)] if a.adaptive else []
+    p64s = []   # the primary pass of --adaptive renders fp64 images (the selection reads fp64 colours)
+    for c in cams:
+        q = rtamd.abi.RenderParams.from_buffer_copy(c)
+        q.out_format = rtamd.RT_OUT_RGB_F64
+        p64s.append(q)
     # N > 1: the neighbour test of a stripe's edge rows needs the rows the neighbouring ranks
     # rendered -- ONE all_gather of every rank's stripe-edge rows per frame (rtamd.shard.HaloExchange)
     halo_x = HaloExchange(a.height, W, STRIPE_H, n, rank, rtamd.adaptive_halo_rows(params), device="cuda",
@@ -177,6 +186,13 @@ def main():
         halo = halo_x(prim[:rows_local])
         return gpu.launch_adaptive_shard(params, prim.data_ptr(), halo.data_ptr(), out.data_ptr(), 4, 0.02,
                                          stats=stats, stream=stream_)
+
+    def adaptive_frames(prim, outs, nf, stats, stream_):
+        """One GPU: the primary passes of nf frames (fp64, one launch), then their adaptive passes
+        (one launch); returns (Stats of the adaptive pass, pixels supersampled)."""
+        gpu.launch_frames(p64s[:nf], [prim[f].data_ptr() for f in range(nf)], stats=False, stream=stream_)
+        return gpu.launch_adaptive_frames(cams[:nf], [prim[f].data_ptr() for f in range(nf)],
+                                          [o.data_ptr() for o in outs[:nf]], 4, 0.02, stats=stats, stream=stream_)
 
     # ---- counters (untimed launches of exactly the timed launch shapes) ----
     # rays of one launch of nf frames (frames cams[:nf]); the timed run is full launches of F frames
@@ -200,11 +216,16 @@ def main():
     tst = launch_counts(F, rtamd.RT_FLAG_TRAVERSAL_STATS)   # canonical 2-wide walk of the reference tree
     wst = launch_counts(F, rtamd.RT_FLAG_WIDE_STATS)        # the production kernel's own fetches
     adaptive_info = None
-    if a.adaptive:   # untimed: rays of the adaptive pass (selection depends on the primary image)
-        p64 = rtamd.abi.RenderParams.from_buffer_copy(params)
-        p64.out_format = rtamd.RT_OUT_RGB_F64
-        gpu.launch(p64, prims[0].data_ptr(), stats=True, stream=stream)
-        ast, nsel = adaptive_pass(prims[0], bufs[0], True, stream)
+    if batched_adaptive:   # untimed: rays of the adaptive passes (selection depends on the primary images)
+        ast, nsel = adaptive_frames(prims[0], bufs, F, True, stream)
+        rays_timed_local += n_full * rays_of(ast) + (rays_of(adaptive_frames(prims[0], bufs, rem, True, stream)[0])
+                                                     if rem else 0)
+        rays_frame0_local += rays_of(adaptive_frames(prims[0], bufs, 1, True, stream)[0])
+        adaptive_info = {"pixels_supersampled_per_frame": round(nsel / F, 1), "subp": 4, "threshold": 0.02,
+                         "rays_per_frame": round(rays_of(ast) / F, 1), "frames_per_launch": F}
+    elif a.adaptive:
+        gpu.launch(p64s[0], prims[0][0].data_ptr(), stats=True, stream=stream)
+        ast, nsel = adaptive_pass(prims[0][0], bufs[0], True, stream)
         rays_timed_local += a.steps * rays_of(ast)
         rays_frame0_local += rays_of(ast)
         adaptive_info = {("pixels_supersampled" if n == 1 else "pixels_supersampled_rank0"): nsel, "subp": 4,
@@ -228,9 +249,11 @@ def main():
             if timed:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(s)
-            if a.adaptive:
-                gpu.launch(p64, prims[li % S].data_ptr(), stats=False, stream=s.cuda_stream)
-                adaptive_pass(prims[li % S], bs[0], False, s.cuda_stream)
+            if batched_adaptive:
+                adaptive_frames(prims[li % S], bs, nf, False, s.cuda_stream)
+            elif a.adaptive:
+                gpu.launch(p64s[0], prims[li % S][0].data_ptr(), stats=False, stream=s.cuda_stream)
+                adaptive_pass(prims[li % S][0], bs[0], False, s.cuda_stream)
             elif nf == 1:
                 gpu.launch(cams[0], bs[0].data_ptr(), stats=False, stream=s.cuda_stream)
             else:

@@ -230,6 +230,18 @@ int rt_launch_frames(rt_scene* scene, const rt_render_params* p, int n_frames, v
 int rt_launch_adaptive(rt_scene* scene, const rt_render_params* p, const double* d_primary, void* d_out, int subp,
                        double threshold, rt_stats* stats, long long* n_selected, void* stream);
 
+/* Adaptive pass over n_frames full frames at once (animation / batched frames):
+ * p[0..n_frames) differ only in their camera vectors (as rt_launch_frames), d_primary[f] is frame
+ * f's fp64 primary image, d_out[f] its output.  Every frame's selection goes into one list and
+ * one launch traces every sample of every selected pixel of every frame (a pixel's samples on
+ * neighbouring lanes, as rt_launch_adaptive), so the per-launch drain is paid once per batch;
+ * the sample buffer is sized by the selection count, which the call reads back (one host
+ * synchronisation per call).  Results equal rt_launch_adaptive on each frame.  W x H < 2^25.
+ * *n_selected (optional) = pixels re-rendered over all frames. */
+int rt_launch_adaptive_frames(rt_scene* scene, const rt_render_params* p, int n_frames, const double* const* d_primary,
+                              void* const* d_out, int subp, double threshold, rt_stats* stats, long long* n_selected,
+                              void* stream);
+
 /* Adaptive pass over a row shard (the multi-GPU case).  p may use
  * stripes or a row range; d_primary / d_out are the shard's packed rows (as
  * rt_launch_compute_image writes them), d_primary in RT_OUT_RGB_F64.  The

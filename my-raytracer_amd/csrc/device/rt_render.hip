@@ -157,6 +157,10 @@ constexpr int kTlCap = 256;   // TL variant: traversal rounds recorded per wave
 constexpr int kTlWords = 8;   // ... and words per round
 
 constexpr int kMaxFrames = RT_MAX_FRAMES;   // frames per launch
+// adaptive-pass list entries: frame << 25 | local pixel id (lrow * W + x)
+constexpr int kListFrameShift = 25;
+constexpr uint32_t kListPixMask = (1u << kListFrameShift) - 1u;
+static_assert(kMaxFrames <= (1 << (32 - kListFrameShift)), "frame index must fit a list entry");
 // per-frame camera and output buffer; a launch's table follows its counters in device memory
 struct FrameDesc {
   double eye[3], ll[3], xd[3], yd[3];
@@ -205,8 +209,9 @@ struct KParams {
   int tiles_x;
   int pad1;
   long long n_tiles;
-  // list mode (adaptive pass): work item w = one sample (w % nsamp) of the shard's (local) pixel
-  // list[w / nsamp]; its trace() colour goes to sample_out[3w..3w+2] (summed in order later)
+  // list mode (adaptive pass): list entries are frame << 25 | local pixel id; work item w = one
+  // sample (w % nsamp) of pixel list[w / nsamp] (a pixel's samples run on neighbouring lanes:
+  // coherent rays); its trace() colour goes to sample_out[3w..3w+2] (summed in order later).
   const uint32_t* list;
   const unsigned long long* list_count;
   double* sample_out;
@@ -578,10 +583,12 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
       if (state == ST_FETCH) {
         const long long wk = start + __popcll(m_fetch & lane_below);
         if (wk < g1) {
-          if (P.list) {   // adaptive pass: one sample of a listed pixel (full frame)
+          if (P.list) {   // adaptive pass: one sample of a listed pixel
             const uint32_t id = wk < n_list ? P.list[wk / P.nsamp] : 0xffffffffu;
-            px = id != 0xffffffffu ? (int)(id % (uint32_t)P.W) : P.W;
-            lrow = id != 0xffffffffu ? (int)(id / (uint32_t)P.W) : P.rows;
+            const uint32_t pix = id & kListPixMask;
+            frame = id != 0xffffffffu ? (int)(id >> kListFrameShift) : 0;
+            px = id != 0xffffffffu ? (int)(pix % (uint32_t)P.W) : P.W;
+            lrow = id != 0xffffffffu ? (int)(pix / (uint32_t)P.W) : P.rows;
             item = wk;
           } else {
             long long tile = wk >> 6;
@@ -1485,7 +1492,7 @@ struct ShardRows {
 __global__ void __launch_bounds__(256) adaptive_select_kernel(const double* prim, const double* halo, void* out,
                                                               int out_fmt, ShardRows G, double threshold,
                                                               int tiles_x, long long n_tiles, uint32_t* list,
-                                                              unsigned long long* count) {
+                                                              unsigned long long* count, uint32_t frame_tag) {
   const long long tile = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int j = threadIdx.x & 63;
   const int W = G.W;
@@ -1526,7 +1533,7 @@ __global__ void __launch_bounds__(256) adaptive_select_kernel(const double* prim
   base = __shfl(base, leader);
   if (sel) {
     const unsigned long long below = lane == 0 ? 0ull : (m & (~0ull >> (64 - lane)));
-    list[base + __popcll(below)] = (uint32_t)((size_t)lrow * W + x);
+    list[base + __popcll(below)] = frame_tag | (uint32_t)((size_t)lrow * W + x);
   }
 }
 
@@ -1534,7 +1541,7 @@ __global__ void __launch_bounds__(256) adaptive_select_kernel(const double* prim
 // samples in (si, sj) order, divide by subp^2, clamp, store.
 __global__ void __launch_bounds__(256) adaptive_reduce_kernel(const uint32_t* list, const unsigned long long* count,
                                                               const double* samples, int nsamp, void* out,
-                                                              int out_fmt) {
+                                                              int out_fmt, const FrameDesc* frames) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long long)*count) return;
   const double* s = samples + 3 * (size_t)i * nsamp;
@@ -1548,7 +1555,9 @@ __global__ void __launch_bounds__(256) adaptive_reduce_kernel(const uint32_t* li
   r = stdmin(r / nn, 1.0);
   g = stdmin(g / nn, 1.0);
   b = stdmin(b / nn, 1.0);
-  const size_t o = 3 * (size_t)list[i];
+  const uint32_t id = list[i];
+  const size_t o = 3 * (size_t)(id & kListPixMask);
+  if (frames) out = frames[id >> kListFrameShift].out;   // several frames: the launch's frame table
   if (out_fmt == RT_OUT_RGB_F64) {
     double* d = reinterpret_cast<double*>(out) + o;
     d[0] = r; d[1] = g; d[2] = b;
@@ -3305,7 +3314,7 @@ int rt_launch_adaptive_shard(rt_scene* sc, const rt_render_params* p, const doub
   const long long n_tiles = (long long)tiles_x * ((G.rows + 7) / 8);
   if (n_tiles > 0) {
     hipLaunchKernelGGL(adaptive_select_kernel, dim3((unsigned)((n_tiles + 3) / 4)), dim3(256), 0, st, d_primary,
-                       d_halo, d_out, p->out_format, G, threshold, tiles_x, n_tiles, list, cnt);
+                       d_halo, d_out, p->out_format, G, threshold, tiles_x, n_tiles, list, cnt, 0u);
     HIP_TRY(hipGetLastError());
   }
   rt_render_params q = *p;
@@ -3313,7 +3322,7 @@ int rt_launch_adaptive_shard(rt_scene* sc, const rt_render_params* p, const doub
   int rc = launch_render(sc, &q, 1, &d_out, stats, stream, list, cnt, cap, samples);
   if (rc == RT_OK && cap > 0) {
     hipLaunchKernelGGL(adaptive_reduce_kernel, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, st, list, cnt,
-                       samples, nsamp, d_out, p->out_format);
+                       samples, nsamp, d_out, p->out_format, nullptr);
     HIP_TRY(hipGetLastError());
   }
   if (rc == RT_OK && n_selected) {
@@ -3335,6 +3344,66 @@ int rt_launch_adaptive(rt_scene* sc, const rt_render_params* p, const double* d_
   if ((p->stripe_count > 1) || p->row_begin != 0 || (p->row_end > 0 && p->row_end != H))
     return fail(RT_ERR_INVALID, "rt_launch_adaptive: needs the full frame (neighbour test), no stripes/row range");
   return rt_launch_adaptive_shard(sc, p, d_primary, nullptr, d_out, subp, threshold, stats, n_selected, stream);
+}
+
+int rt_launch_adaptive_frames(rt_scene* sc, const rt_render_params* p, int n_frames, const double* const* d_primary,
+                              void* const* d_out, int subp, double threshold, rt_stats* stats, long long* n_selected,
+                              void* stream) {
+  if (!sc || !p || !d_primary || !d_out) return fail(RT_ERR_INVALID, "rt_launch_adaptive_frames: null argument");
+  if (n_frames < 1 || n_frames > kMaxFrames) return fail(RT_ERR_INVALID, "rt_launch_adaptive_frames: n_frames out of range");
+  if (subp < 1 || subp > 64) return fail(RT_ERR_INVALID, "rt_launch_adaptive_frames: subp must be in [1, 64]");
+  if (n_frames == 1)
+    return rt_launch_adaptive(sc, p, d_primary[0], d_out[0], subp, threshold, stats, n_selected, stream);
+  const int W = p->camera.width, H = p->camera.height;
+  if (W <= 0 || H <= 0) return fail(RT_ERR_INVALID, "bad image size");
+  if ((long long)W * H > (long long)kListPixMask) return fail(RT_ERR_INVALID, "rt_launch_adaptive_frames: frame too large");
+  if (p->out_format != RT_OUT_RGB_F32 && p->out_format != RT_OUT_RGB_F64) return fail(RT_ERR_INVALID, "bad out_format");
+  if ((p->stripe_count > 1) || p->row_begin != 0 || (p->row_end > 0 && p->row_end != H))
+    return fail(RT_ERR_INVALID, "rt_launch_adaptive_frames: needs full frames (neighbour test), no stripes/row range");
+  for (int f = 0; f < n_frames; ++f)
+    if (!d_primary[f] || !d_out[f]) return fail(RT_ERR_INVALID, "rt_launch_adaptive_frames: null frame buffer");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  HIP_TRY(hipSetDevice(sc->device));
+  const ShardRows G = shard_rows_of(p);
+  const long long per = (long long)std::max(0, W - 2) * G.rows;   // interior pixels only can be selected
+  const long long cap = per * n_frames;
+  uint32_t* list = nullptr;
+  unsigned long long* cnt = nullptr;
+  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&list), (size_t)std::max(1LL, cap) * sizeof(uint32_t), st));
+  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&cnt), sizeof(unsigned long long), st));
+  HIP_TRY(hipMemsetAsync(cnt, 0, sizeof(unsigned long long), st));
+  const int tiles_x = (W + 7) / 8;
+  const long long n_tiles = (long long)tiles_x * ((G.rows + 7) / 8);
+  for (int f = 0; f < n_frames && n_tiles > 0; ++f) {   // every frame's selection into one list
+    hipLaunchKernelGGL(adaptive_select_kernel, dim3((unsigned)((n_tiles + 3) / 4)), dim3(256), 0, st, d_primary[f],
+                       nullptr, d_out[f], p->out_format, G, threshold, tiles_x, n_tiles, list, cnt,
+                       (uint32_t)f << kListFrameShift);
+    HIP_TRY(hipGetLastError());
+  }
+  // every sample of every selected pixel of every frame in one launch: the sample buffer is sized
+  // by the selection count (read back: one synchronisation per batch)
+  unsigned long long n_sel = 0;
+  HIP_TRY(hipMemcpyAsync(&n_sel, cnt, sizeof n_sel, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  const int nsamp = subp * subp;
+  double* samples = nullptr;
+  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&samples),
+                         (size_t)std::max(1ull, n_sel) * nsamp * 3 * sizeof(double), st));
+  std::vector<rt_render_params> q(p, p + n_frames);
+  for (auto& x : q) x.spp_n = subp;
+  int rc = launch_render(sc, q.data(), n_frames, d_out, stats, stream, list, cnt, (long long)n_sel, samples);
+  if (rc == RT_OK && n_sel > 0) {   // sums in (si, sj) order into each frame's output (that launch's frame table)
+    const FrameDesc* table = reinterpret_cast<const FrameDesc*>(
+        reinterpret_cast<const unsigned char*>(sc->ctx[sc->last_ctx].d_ctr) + kCtrBytes);
+    hipLaunchKernelGGL(adaptive_reduce_kernel, dim3((unsigned)((n_sel + 255) / 256)), dim3(256), 0, st, list, cnt,
+                       samples, nsamp, nullptr, p->out_format, table);
+    HIP_TRY(hipGetLastError());
+  }
+  if (n_selected) *n_selected = (long long)n_sel;
+  (void)hipFreeAsync(list, st);
+  (void)hipFreeAsync(cnt, st);
+  (void)hipFreeAsync(samples, st);
+  return rc;
 }
 
 int rt_render_to_host(rt_scene* sc, const rt_render_params* p, void* host_out, rt_stats* stats) {

@@ -278,6 +278,25 @@ class DeviceScene:
                    "rt_launch_adaptive")
         return st, int(nsel.value)
 
+    def launch_adaptive_frames(self, params, d_primaries, d_outs, subp=4, threshold=0.02, stats=False, stream=None):
+        """Adaptive pass over len(d_outs) full frames in one render launch (rt_launch_adaptive_frames);
+        params as launch_frames.  Returns (Stats or None, re-rendered pixels over all frames)."""
+        n = len(d_outs)
+        plist = params if isinstance(params, (list, tuple)) else [params] * n
+        if len(plist) != n or len(d_primaries) != n:
+            raise ValueError("one params and one primary image per output buffer")
+        parr = (abi.RenderParams * n)(*plist)
+        parr_p = (C.c_void_p * n)(*[C.c_void_p(d) for d in d_primaries])
+        oarr = (C.c_void_p * n)(*[C.c_void_p(d) for d in d_outs])
+        st = abi.Stats() if stats else None
+        nsel = C.c_longlong(-1)
+        _check_hip(hip_lib().rt_launch_adaptive_frames(self._h, parr, n, parr_p, oarr, subp, threshold,
+                                                       C.byref(st) if st is not None else None,
+                                                       C.byref(nsel) if stats else None,
+                                                       C.c_void_p(stream) if stream else None),
+                   "rt_launch_adaptive_frames")
+        return st, int(nsel.value)
+
     def launch_adaptive_shard(self, params, d_primary, d_halo, d_out, subp=4, threshold=0.02, stats=False,
                               stream=None):
         """Adaptive pass over a row shard (rt_launch_adaptive_shard): d_primary / d_out are the

@@ -158,6 +158,9 @@ HIP_SYMBOLS = {
     "rt_launch_adaptive_shard": (C.c_int, [C.c_void_p, C.POINTER(RenderParams), C.c_void_p, C.c_void_p,
                                            C.c_void_p, C.c_int, C.c_double, C.POINTER(Stats),
                                            C.POINTER(C.c_longlong), C.c_void_p]),
+    "rt_launch_adaptive_frames": (C.c_int, [C.c_void_p, C.POINTER(RenderParams), C.c_int, C.POINTER(C.c_void_p),
+                                            C.POINTER(C.c_void_p), C.c_int, C.c_double, C.POINTER(Stats),
+                                            C.POINTER(C.c_longlong), C.c_void_p]),
     "rt_adaptive_halo_rows": (C.c_int, [C.POINTER(RenderParams), C.POINTER(C.c_int), C.c_int]),
     "rt_render_to_host": (C.c_int, [C.c_void_p, C.POINTER(RenderParams), C.c_void_p, C.POINTER(Stats)]),
     "rt_last_kernel_ms": (C.c_int, [C.c_void_p, C.POINTER(C.c_float)]),

@@ -65,8 +65,9 @@ def test_bench_adaptive_pass_runs():
                        capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     d = json.loads(r.stdout.strip().splitlines()[-1])
-    ad = d["config"]["adaptive_pass"]
-    assert ad["pixels_supersampled"] > 0 and ad["rays"] > 0 and d["value"] > 0
+    ad = d["config"]["adaptive_pass"]   # one GPU: the 3 frames' passes batched (rt_launch_adaptive_frames)
+    assert ad["frames_per_launch"] == 3 and d["config"]["frames_per_launch"] == 3
+    assert ad["pixels_supersampled_per_frame"] > 0 and ad["rays_per_frame"] > 0 and d["value"] > 0
 
 
 def test_bench_two_ranks_rehearsal(tmp_path):

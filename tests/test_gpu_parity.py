@@ -372,6 +372,46 @@ def test_adaptive_pass_matches_oracle(kind, kw, w, h):
         assert counts(st) == [cnt.primary_rays, cnt.shadow_rays, cnt.reflection_rays]
 
 
+@pytest.mark.parametrize("kind,w,h", [("office", 96, 54), ("cornell", 64, 48)])
+def test_adaptive_frames_equal_single_frame_passes(kind, w, h):
+    # rt_launch_adaptive_frames: three frames of a camera orbit in one render launch (one lane per
+    # selected pixel, all 16 samples in order) must give each frame's single-frame pass bit for bit
+    # (per-sample work items, summed by the reduce kernel), selections and ray counts adding up;
+    # frame 0 is also checked against the oracle.
+    import torch
+
+    hs, dev, orc = Case.get(kind)
+    p = hs.render_params(w, h, 1)
+    cams = [rtamd.camera_orbit(p, a) for a in (-0.05, 0.0, 0.07)]
+    prims, singles, sel_sum, cnt_sum = [], [], 0, [0, 0, 0]
+    for q in cams:
+        q64 = rtamd.abi.RenderParams.from_buffer_copy(q)
+        q64.out_format = rtamd.RT_OUT_RGB_F64
+        prim = torch.zeros((h, w, 3), dtype=torch.float64, device="cuda")
+        dev.launch(q64, prim.data_ptr(), stats=True)
+        out = torch.zeros((h, w, 3), dtype=torch.float64, device="cuda")
+        st, nsel = dev.launch_adaptive(q64, prim.data_ptr(), out.data_ptr(), 4, 0.02, stats=True)
+        prims.append(prim)
+        singles.append(out.cpu().numpy())
+        sel_sum += nsel
+        cnt_sum = [a + b for a, b in zip(cnt_sum, counts(st))]
+    assert sel_sum > 0
+    q64s = []
+    for q in cams:
+        q64 = rtamd.abi.RenderParams.from_buffer_copy(q)
+        q64.out_format = rtamd.RT_OUT_RGB_F64
+        q64s.append(q64)
+    outs = [torch.zeros((h, w, 3), dtype=torch.float64, device="cuda") for _ in cams]
+    st, nsel = dev.launch_adaptive_frames(q64s, [x.data_ptr() for x in prims], [o.data_ptr() for o in outs],
+                                          4, 0.02, stats=True)
+    assert nsel == sel_sum
+    assert counts(st) == cnt_sum
+    for o, ref in zip(outs, singles):
+        assert np.array_equal(o.cpu().numpy(), ref)
+    ref0, c0, sel0 = orc.adaptive(q64s[0], prims[0].cpu().numpy(), subp=4, threshold=0.02)
+    assert np.abs(singles[0] - ref0).max() <= TOL64
+
+
 def test_adaptive_end_to_end_and_full_frame_only():
     hs, dev, orc = Case.get("office")
     p = hs.render_params(128, 72, 1)
