@@ -58,7 +58,7 @@ def hip_lib():
         _one_hip_runtime()
         if not HIP_LIB.exists():
             raise RtError(f"{HIP_LIB} not built: run `make -C my-raytracer_amd` or __graft_entry__.build()")
-        _hip = abi.bind(C.CDLL(str(HIP_LIB)), abi.HIP_SYMBOLS)
+        _hip = abi.bind(C.CDLL(str(HIP_LIB)), abi.HIP_SYMBOLS, partial="RTAMD_HIP_LIB" in os.environ)
     return _hip
 
 

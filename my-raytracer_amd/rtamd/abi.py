@@ -207,10 +207,10 @@ MULTI_SYMBOLS = {
 }
 
 
-def bind(lib, table):
+def bind(lib, table, partial=False):
     for name, (res, args) in table.items():
-        if name.startswith("rt_debug_") and not hasattr(lib, name):
-            continue   # diagnostics a kernel variant library built from an older source lacks (A/B tools)
+        if (partial or name.startswith("rt_debug_")) and not hasattr(lib, name):
+            continue   # entry points a kernel variant built from an older source lacks (A/B tools)
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
