@@ -393,8 +393,13 @@ __device__ __forceinline__ uint32_t u4c(const uint4& v, int c) {
 #define RT_WAVES_PER_EU 4   // 4 waves/SIMD = 16 waves/CU (register budget 128 VGPRs)
 #endif
 
-template <int WIDTH, bool STATS, bool TL = false>
+// RING: entries of the per-lane traversal-stack ring in LDS (8: room for the 73-node treelet;
+// 16: deep hierarchies, e.g. millions of random triangles, which spill an 8-entry ring often;
+// the treelet then gets what is left, 9 nodes -- rt_scene picks per scene)
+template <int WIDTH, bool STATS, bool TL = false, int RING = kShortStack>
 __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render_kernel(KParams P) {
+  static_assert(RING >= kMigWords && (RING & (RING - 1)) == 0, "ring: a power of two holding the migration words");
+  constexpr int kRingMask = RING - 1;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   double* lds_d = reinterpret_cast<double*>(lds_raw);
   RaySlots R;
@@ -752,19 +757,19 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
       // logical stack [0, sp); the LDS ring holds [slo, sp), spill[] holds [0, slo)
       int sp = 0, slo = 0;
       auto push = [&](uint32_t x) {
-        if (sp - slo == kShortStack) {
-          spill[(size_t)slo * P.nslots] = stk[(slo & kStackMask) * kBlock];
+        if (sp - slo == RING) {
+          spill[(size_t)slo * P.nslots] = stk[(slo & kRingMask) * kBlock];
           slo++;
           if (STATS) d_spills++;
           if constexpr (TL) tl_spill++;
         }
-        stk[(sp & kStackMask) * kBlock] = x;
+        stk[(sp & kRingMask) * kBlock] = x;
         sp++;
       };
       auto pop = [&]() -> uint32_t {
         if (sp == 0) return kDone;
         --sp;
-        if (sp >= slo) return stk[(sp & kStackMask) * kBlock];
+        if (sp >= slo) return stk[(sp & kRingMask) * kBlock];
         slo = sp;
         return spill[(size_t)sp * P.nslots];
       };
@@ -1604,25 +1609,34 @@ struct Variant {
 
 // [0] production (4-wide), [1] 4-wide + counters, [2] canonical 2-wide counters
 // (the traversal the oracle replicates: tests pin its node / triangle counts),
-// [3] production + per-round timeline (RT_FLAG_TIMELINE, diagnostics).
+// [3] production + per-round timeline (RT_FLAG_TIMELINE, diagnostics), [4] production with a
+// 16-entry stack ring (deep hierarchies).
 const Variant kVariants[] = {
     {render_kernel<4, false>, false},
     {render_kernel<4, true>, true},
     {render_kernel<2, true>, true},
     {render_kernel<4, false, true>, false},
+    {render_kernel<4, false, false, 16>, false},
 };
-constexpr int kNumVariants = 4;
+constexpr int kNumVariants = 5;
+constexpr int kRingDeep = 16;
+inline int variant_ring(int v) { return v == 4 ? kRingDeep : kShortStack; }
 constexpr int kMaxDepth = 4096;  // traversal stack entries (LDS ring + global spill)
 // LDS per block: kSlotDoubles doubles of slot, task + visibility words and
-// min(stack_words, kShortStack) stack entries per thread.
-size_t lds_bytes(int stack_words) {
+// min(stack_words, ring) stack entries per thread.
+size_t lds_bytes(int stack_words, int ring = kShortStack) {
   stack_words = std::max(stack_words, kMigWords);   // compaction hands registers over in stack entries
   return (size_t)kBlock *
-         (kSlotDoubles * sizeof(double) + (2 + (size_t)std::min(stack_words, kShortStack)) * sizeof(uint32_t));
+         (kSlotDoubles * sizeof(double) + (2 + (size_t)std::min(stack_words, ring)) * sizeof(uint32_t));
 }
 // ... plus the top treelet (n_top 128-B nodes) after it
-size_t lds_bytes_total(int stack_words, int n_top) {
-  return lds_bytes(stack_words) + (size_t)n_top * sizeof(GNode4) + RT_MAX_LIGHTS * 6 * sizeof(double) + kPoolBytes;
+size_t lds_bytes_total(int stack_words, int n_top, int ring = kShortStack) {
+  return lds_bytes(stack_words, ring) + (size_t)n_top * sizeof(GNode4) + RT_MAX_LIGHTS * 6 * sizeof(double) + kPoolBytes;
+}
+// treelet nodes that fit next to a ring of the given size in a block's 40 KB
+int top_nodes_for(int stack_words, int ring, int n_gnodes4) {
+  const long long room = 40960 - (long long)lds_bytes_total(stack_words, 0, ring);
+  return (int)std::max(0LL, std::min<long long>({room / (long long)sizeof(GNode4), (long long)kTopNodes, (long long)n_gnodes4}));
 }
 
 }  // namespace
@@ -1673,7 +1687,9 @@ struct rt_scene {
   double root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};
   long long bytes = 0;
   int n_cu = 0;
-  int blocks_per_cu[kNumVariants] = {0, 0, 0, 0};
+  int blocks_per_cu[kNumVariants] = {0, 0, 0, 0, 0};
+  bool deep = false;            // launches use the 16-entry ring variant (deep hierarchy)
+  int n_top_deep = 0;           // treelet nodes beside the 16-entry ring
   GNode4* d_nodes4 = nullptr;
   int n_gnodes4 = 0;
   int n_top = 0;                // 4-wide nodes each block caches in LDS
@@ -2936,6 +2952,12 @@ int upload_image(const SceneImage& I, int device, rt_scene** out) {
   sc->n_top = RT_TOP_NODES > 0 ? std::min(kTopNodes, sc->n_gnodes4) : 0;
   if (const char* e = std::getenv("RT_LDS_TOP"))   // A/B knob: cache fewer nodes (0 = none)
     sc->n_top = std::max(0, std::min(sc->n_top, std::atoi(e)));
+  // deep hierarchies (half a million device records and more: random-triangle soups of ~1 M and
+  // up spill an 8-entry ring on every other ray, the office proxy on 1 in 130) render with the
+  // 16-entry ring and the 9-node treelet that fits beside it (A/B)
+  sc->deep = I.tris.size() >= (size_t)(1u << 19);
+  if (const char* e = std::getenv("RT_RING")) sc->deep = std::atoi(e) >= 16;   // A/B knob
+  sc->n_top_deep = RT_TOP_NODES > 0 ? top_nodes_for(sc->stack_words, kRingDeep, sc->n_gnodes4) : 0;
   sc->delta = I.delta;
   for (int k = 0; k < 3; ++k) {
     sc->root_lo[k] = I.root_lo[k];
@@ -2945,9 +2967,10 @@ int upload_image(const SceneImage& I, int device, rt_scene** out) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) { rt_scene_free(sc); return fail(RT_ERR_HIP, "hipGetDeviceProperties failed"); }
   sc->n_cu = prop.multiProcessorCount;
-  const size_t lds = lds_bytes_total(sc->stack_words, sc->n_top);
   int max_blocks = 1;
   for (int v = 0; v < kNumVariants; ++v) {
+    const int ring = variant_ring(v);
+    const size_t lds = lds_bytes_total(sc->stack_words, ring == kRingDeep ? sc->n_top_deep : sc->n_top, ring);
     int nb = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(kVariants[v].fn), kBlock, lds) !=
             hipSuccess || nb < 1)
@@ -3168,11 +3191,14 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
 
   const int v = (p->flags & RT_FLAG_TRAVERSAL_STATS) ? 2
                 : (p->flags & RT_FLAG_WIDE_STATS) ? 1
-                : (p->flags & RT_FLAG_TIMELINE) ? 3 : 0;
-  const size_t lds = lds_bytes_total(sc->stack_words, sc->n_top);
-  P.n_top = sc->n_top;
-  P.top_off = (int)lds_bytes(sc->stack_words);
-  P.lights_off = P.top_off + sc->n_top * (int)sizeof(GNode4);
+                : (p->flags & RT_FLAG_TIMELINE) ? 3
+                : sc->deep ? 4 : 0;   // 4: the 16-entry-ring production variant
+  const int ring = variant_ring(v);
+  const int n_top = ring == kRingDeep ? sc->n_top_deep : sc->n_top;
+  const size_t lds = lds_bytes_total(sc->stack_words, n_top, ring);
+  P.n_top = n_top;
+  P.top_off = (int)lds_bytes(sc->stack_words, ring);
+  P.lights_off = P.top_off + n_top * (int)sizeof(GNode4);
   P.pool_off = P.lights_off + RT_MAX_LIGHTS * 6 * (int)sizeof(double);
   const long long waves_needed = (P.n_tiles * 64 + 63) / 64;
   int bpc = sc->blocks_per_cu[v];

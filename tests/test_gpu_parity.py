@@ -644,6 +644,28 @@ def test_tree_independent_of_build_threads(monkeypatch, tree):
     assert np.array_equal(out[0][0], out[1][0]) and out[0][1:] == out[1][1:]
 
 
+@pytest.mark.parametrize("kind,kw,w,h,spp", [("office", {}, 320, 180, 1), ("cornell", {"detail": 3}, 97, 61, 2),
+                                             ("random_tris", {"n_triangles": 200000}, 160, 90, 1)])
+def test_stack_ring_depth_changes_no_pixel(monkeypatch, kind, kw, w, h, spp):
+    # Scenes of >= 2^19 triangles launch the 16-entry LDS stack ring (fewer global spills on deep
+    # trees, a smaller LDS treelet); RT_RING forces either ring on any scene.  Same bits, same
+    # ray counts, and the deep ring still matches the oracle.
+    hs, _, orc = Case.get(kind, **kw)
+    p = hs.render_params(w, h, spp)
+    p.out_format = rtamd.RT_OUT_RGB_F64
+    out = []
+    for ring in ("8", "16"):
+        monkeypatch.setenv("RT_RING", ring)
+        dev = rtamd.DeviceScene(hs, 0)
+        out.append(dev.render(p))
+        dev.close()
+    (a, sa), (b, sb) = out
+    assert np.array_equal(a, b) and counts(sa) == counts(sb)
+    ref, cnt = orc.render(p, pyoracle.MODE_ORDERED, threads=0)
+    assert np.abs(b - ref).max() <= TOL64
+    assert counts(sb) == [cnt.primary_rays, cnt.shadow_rays, cnt.reflection_rays]
+
+
 def test_unknown_device_tree_fails_loudly():
     hs, _, _ = Case.get("cornell")
     with pytest.raises(ValueError):
