@@ -23,8 +23,8 @@ from collections import defaultdict
 
 
 def is_production(name):
-    # render_kernel<4, false> (round 1) / render_kernel<4, false, false> (mangled ...ILi4ELb0ELb0E...)
-    return "render_kernel" in name and ("<4, false>" in name or "<4, false, false>" in name
+    # render_kernel<4, false> (round 1) / render_kernel<4, false, false[, RING]> (mangled ...ILi4ELb0ELb0E...)
+    return "render_kernel" in name and ("<4, false>" in name or "<4, false, false" in name
                                         or "ILi4ELb0EEE" in name or "ILi4ELb0ELb0E" in name)
 
 

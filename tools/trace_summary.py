@@ -25,7 +25,7 @@ def main():
         with open(p) as f:
             for r in csv.DictReader(f):
                 name = r["Kernel_Name"]
-                if any(k in name for k in ("render_kernel<4, false>", "render_kernel<4, false, false>",
+                if any(k in name for k in ("render_kernel<4, false>", "render_kernel<4, false, false",
                                            "ILi4ELb0EEE", "ILi4ELb0ELb0E")):
                     rows.append((int(r["Start_Timestamp"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6))
     rows.sort()
