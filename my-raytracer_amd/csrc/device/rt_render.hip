@@ -2547,7 +2547,7 @@ extern "C" {
 const char* rt_last_error(void) { return g_error.c_str(); }
 
 const char* rt_build_info(void) {
-  return "librt_hip: gfx950 persistent flattened render kernel; variants {4-wide 8-entry stack ring, 4-wide 16-entry ring (>= 2^19 triangles), "
+  return "librt_hip: gfx950 persistent flattened render kernel; variants {4-wide 8-entry stack ring, 4-wide 16-entry ring (>= 2^18 triangle records), "
          "4-wide+stats, 2-wide canonical stats, 4-wide+round timeline}; fp32 4-wide nodes (128 B) with an LDS treelet, "
          "fp64 triangles/shading, LDS ray slots + stack ring (global spill), global path state, 8 XCD work heads";
 }
@@ -2956,7 +2956,7 @@ int upload_image(const SceneImage& I, int device, rt_scene** out) {
   // deep hierarchies (half a million device records and more: random-triangle soups of ~1 M and
   // up spill an 8-entry ring on every other ray, the office proxy on 1 in 130) render with the
   // 16-entry ring and the 9-node treelet that fits beside it (A/B)
-  sc->deep = I.tris.size() >= (size_t)(1u << 19);
+  sc->deep = I.tris.size() >= (size_t)(1u << 18);   // device records (office 77 k prefers 8, 500 k random 16)
   if (const char* e = std::getenv("RT_RING")) sc->deep = std::atoi(e) >= 16;   // A/B knob
   sc->n_top_deep = RT_TOP_NODES > 0 ? top_nodes_for(sc->stack_words, kRingDeep, sc->n_gnodes4) : 0;
   sc->delta = I.delta;

@@ -647,7 +647,7 @@ def test_tree_independent_of_build_threads(monkeypatch, tree):
 @pytest.mark.parametrize("kind,kw,w,h,spp", [("office", {}, 320, 180, 1), ("cornell", {"detail": 3}, 97, 61, 2),
                                              ("random_tris", {"n_triangles": 200000}, 160, 90, 1)])
 def test_stack_ring_depth_changes_no_pixel(monkeypatch, kind, kw, w, h, spp):
-    # Scenes of >= 2^19 triangles launch the 16-entry LDS stack ring (fewer global spills on deep
+    # Scenes of >= 2^18 device triangle records launch the 16-entry LDS stack ring (fewer global spills on deep
     # trees, a smaller LDS treelet); RT_RING forces either ring on any scene.  Same bits, same
     # ray counts, and the deep ring still matches the oracle.
     hs, _, orc = Case.get(kind, **kw)
