@@ -3208,6 +3208,8 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   long long blocks = (long long)sc->n_cu * bpc;
   blocks = std::max<long long>(1, std::min<long long>(blocks, (waves_needed + kBlock / 64 - 1) / (kBlock / 64)));
   blocks = std::min<long long>(blocks, (long long)(sc->nslots / kBlock));
+  if (const char* e = std::getenv("RT_GRID_SPARE"))   // A/B knob: leave block slots to concurrent kernels
+    blocks = std::max<long long>(1, blocks - std::max(0, std::atoi(e)));
 
   if (C.used) {
     HIP_TRY(hipStreamWaitEvent(st, C.ev1, 0));   // previous launch on this context done (device side)

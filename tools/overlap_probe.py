@@ -1,30 +1,47 @@
-"""Throughput of back-to-back frames on one stream vs alternating two streams with
-two device scenes (independent launch state) -- does the per-launch drain hide? (dev tool)"""
+"""Can another kernel run beside the persistent render kernel? (dev tool, under gpurun)  Stream A
+renders a 32-frame launch; stream B, enqueued right after, copies 1 GB device to device (a
+stand-in for the RCCL gather of the previous launch).  Prints, per RT_GRID_SPARE setting, when B
+ends relative to A's start and end (ms)."""
+import json
+import os
 import sys
-import time
 
 import torch
 
 sys.path.insert(0, "my-raytracer_amd")
 import rtamd  # noqa: E402
 
-w, h = (int(a) for a in (sys.argv[1:3] if len(sys.argv) > 2 else (1920, 1080)))
-K = 20
 host = rtamd.HostScene.generate("office")
 host.prepare()
-scenes = [rtamd.DeviceScene(host, 0) for _ in range(3)]
-p = host.render_params(w, h, 1)
-st = scenes[0].launch(p, torch.zeros(h * w * 3, device="cuda").data_ptr(), stats=True)
-rays = st.primary_rays + st.shadow_rays + st.reflection_rays
-for nstreams in (1, 2, 3):
-    streams = [torch.cuda.Stream() for _ in range(nstreams)]
-    bufs = [torch.zeros(h * w * 3, device="cuda") for _ in range(nstreams)]
-    for rep in range(2):
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for k in range(K):
-            i = k % nstreams
-            scenes[i].launch(p, bufs[i].data_ptr(), stats=False, stream=streams[i].cuda_stream)
-        torch.cuda.synchronize()
-        dt = (time.perf_counter() - t0) / K
-    print(f"{w}x{h} streams {nstreams}: {dt*1e3:.3f} ms/frame  {rays/dt/1e6:.0f} Mrays/s", flush=True)
+gpu = rtamd.DeviceScene(host, 0)
+p = host.render_params(1920, 1080, 1)
+F = 32
+out = [torch.zeros((1080, 1920, 3), device="cuda") for _ in range(F)]
+cams = [rtamd.camera_orbit(p, 0.12 * (f / (F - 1) - 0.5)) for f in range(F)]
+x = torch.ones(256 * 1024 * 1024, device="cuda")
+y = torch.empty_like(x)
+sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+res = {}
+for spare in [0, 4, 16, 64, 0, 4, 16, 64]:
+    os.environ["RT_GRID_SPARE"] = str(spare)
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    with torch.cuda.stream(sa):
+        ev[0].record(sa)
+        gpu.launch_frames(cams, [o.data_ptr() for o in out], stream=sa.cuda_stream)
+        ev[1].record(sa)
+    with torch.cuda.stream(sb):
+        sb.wait_event(ev[0])
+        ev[2].record(sb)
+        y.copy_(x)
+        ev[3].record(sb)
+    torch.cuda.synchronize()
+    a_end = ev[0].elapsed_time(ev[1])
+    b_end = ev[0].elapsed_time(ev[3])
+    # alone: the copy by itself
+    with torch.cuda.stream(sb):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(sb); y.copy_(x); e1.record(sb)
+    torch.cuda.synchronize()
+    res.setdefault(spare, []).append((round(a_end, 3), round(b_end, 3), round(e0.elapsed_time(e1), 3)))
+print(json.dumps({str(k): v for k, v in res.items()}), flush=True)
