@@ -17,6 +17,7 @@ from pathlib import Path
 import numpy as np
 import pytest
 
+import fuzz_scenes
 import kat_scenes
 import pyoracle
 import rtamd
@@ -794,3 +795,37 @@ def test_spatial_splits_stress_scene_bit_identical(tmp_path, monkeypatch):
     ref, cnt = pyoracle.Oracle(hs.raw, hs).render(p, pyoracle.MODE_REFERENCE)
     assert np.abs(out["sbvh"][0] - ref).max() <= TOL64
     assert out["sbvh"][1] == counts(cnt)
+
+
+# ---- seeded random scenes (tests/fuzz_scenes.py; the oracle side: tests/test_fuzz_oracle.py) ----
+@pytest.mark.parametrize("seed", range(40))
+def test_fuzz_scene_matches_oracle(tmp_path, seed):
+    # Random meshes, materials, 1-33 lights and depth 0-5 through the loader: the production
+    # kernel (spatial-split hierarchy) within 1e-12 of the oracle's reference-semantics render,
+    # ray counts exact; every 4th seed also walks the refined reference tree (same bits) and
+    # checks the fp32 output and a 3-stripe shard.
+    hs = rtamd.HostScene.load(fuzz_scenes.write(tmp_path, seed, 64, 48))
+    hs.prepare()
+    orc = pyoracle.Oracle(hs.raw, hs)
+    spp = 2 if seed % 4 == 3 else 1
+    p = hs.render_params(0, 0, spp)
+    ref, cnt = orc.render(p, pyoracle.MODE_REFERENCE)
+    p.out_format = rtamd.RT_OUT_RGB_F64
+    dev = rtamd.DeviceScene(hs, 0)
+    img, st = dev.render(p)
+    assert np.abs(img - ref).max() <= TOL64
+    assert counts(st) == [cnt.primary_rays, cnt.shadow_rays, cnt.reflection_rays]
+    dev.close()
+    if seed % 4 == 0:
+        devr = rtamd.DeviceScene(hs, 0, tree="reference")
+        imgr, str_ = devr.render(p)
+        assert np.array_equal(imgr, img) and counts(str_) == counts(st)
+        p.out_format = rtamd.RT_OUT_RGB_F32
+        img32, _ = devr.render(p)
+        assert np.abs(img32.astype(np.float64) - ref).max() <= TOL32
+        p.out_format = rtamd.RT_OUT_RGB_F64
+        p.stripe_height, p.stripe_count, p.stripe_index = 4, 3, 1
+        img3, _ = devr.render(p)
+        rows = [y for y in range(48) if (y // 4) % 3 == 1]
+        assert np.array_equal(img3, img[rows])
+        devr.close()
