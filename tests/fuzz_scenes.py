@@ -89,3 +89,28 @@ def mini(seed, width=9, height=7):
     meshes, lights, cam, bg, amb, depth = scene(seed, width, height)
     eye, center, up, fovy, w, h = cam
     return minirt.Scene(meshes, lights, minirt.camera(eye, center, up, fovy, w, h), bg, amb, depth)
+
+
+def write_analytic(tmpdir, seed, width=64, height=48):
+    """The seed's mesh scene plus 1-4 spheres and 0-2 planes (opt-in GPU analytic path): spheres
+    cutting through meshes, mirror spheres, a tilted reflective plane."""
+    path = write(tmpdir, seed, width, height)
+    rng = random.Random(10_000 + seed)
+    r = lambda v: " ".join(repr(float(x)) for x in v)  # noqa: E731
+
+    def mat():
+        ka, kd, ks, shin, mirror, sh = _mat(rng)
+        return f"{r(ka)}  {r(kd)}  {r(ks)}  {float(shin)!r}  {float(mirror)!r}  {int(sh)}"
+
+    lines = [f"sphere {r([rng.uniform(-1.2, 1.2), rng.uniform(-0.8, 1.0), rng.uniform(-1.2, 1.2)])}  "
+             f"{rng.uniform(0.15, 0.7)!r}  {mat()}" for _ in range(rng.randint(1, 4))]
+    for _ in range(rng.randint(0, 2)):
+        n = [rng.uniform(-0.3, 0.3), 1.0, rng.uniform(-0.3, 0.3)] if rng.random() < 0.5 else \
+            [rng.uniform(-1, 1), rng.uniform(-0.2, 0.2), -1.0]
+        ln = math.sqrt(sum(c * c for c in n))
+        n = [c / ln for c in n]
+        q = [rng.uniform(-0.5, 0.5), rng.uniform(-1.6, -1.0), rng.uniform(-3.5, -2.0)]
+        lines.append(f"plane {r(q)}  {r(n)}  {mat()}")
+    with open(path, "a") as f:
+        f.write("\n".join(lines) + "\n")
+    return path

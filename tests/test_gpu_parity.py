@@ -829,3 +829,30 @@ def test_fuzz_scene_matches_oracle(tmp_path, seed):
         rows = [y for y in range(48) if (y // 4) % 3 == 1]
         assert np.array_equal(img3, img[rows])
         devr.close()
+
+
+@pytest.mark.parametrize("seed", range(0, 40, 3))
+def test_fuzz_analytic_scene_matches_oracle(tmp_path, seed):
+    # the same random scenes plus spheres and planes, opt-in analytic path (CPU intersect_scene
+    # semantics), and the adaptive supersampling pass on top of the fp64 primary image
+    hs = rtamd.HostScene.load(fuzz_scenes.write_analytic(tmp_path, seed, 64, 48))
+    hs.prepare()
+    assert hs.raw.contents.n_spheres >= 1
+    orc = pyoracle.Oracle(hs.raw, hs)
+    dev = rtamd.DeviceScene(hs, 0, analytic=True)
+    p = hs.render_params(0, 0, 1)
+    ref, cnt = orc.render(p, pyoracle.MODE_REFERENCE)
+    p.out_format = rtamd.RT_OUT_RGB_F64
+    img, st = dev.render(p)
+    assert np.abs(img - ref).max() <= TOL64
+    assert counts(st) == [cnt.primary_rays, cnt.shadow_rays, cnt.reflection_rays]
+    import torch
+
+    want, acnt, sel = orc.adaptive(p, img, subp=4, threshold=0.02)
+    prim = torch.from_numpy(img).cuda()
+    out = torch.zeros_like(prim)
+    ast, nsel = dev.launch_adaptive(p, prim.data_ptr(), out.data_ptr(), 4, 0.02, stats=True)
+    assert nsel == int(sel.sum())
+    assert np.abs(out.cpu().numpy() - want).max() <= TOL64
+    assert counts(ast) == [acnt.primary_rays, acnt.shadow_rays, acnt.reflection_rays]
+    dev.close()
