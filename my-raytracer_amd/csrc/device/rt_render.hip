@@ -1508,7 +1508,13 @@ constexpr int kSelTilesPerBlock = (kSelThreads / 64) * kSelTilesPerWave;
 __global__ void __launch_bounds__(kSelThreads) adaptive_select_kernel(const double* prim, const double* halo, void* out,
                                                                       int out_fmt, ShardRows G, double threshold,
                                                                       int tiles_x, long long n_tiles, uint32_t* list,
-                                                                      unsigned long long* count, uint32_t frame_tag) {
+                                                                      unsigned long long* count, uint32_t frame_tag,
+                                                                      const double* const* prims, void* const* outs) {
+  if (prims) {   // several frames in one launch: frame blockIdx.y
+    prim = prims[blockIdx.y];
+    out = outs[blockIdx.y];
+    frame_tag = (uint32_t)blockIdx.y << kListFrameShift;
+  }
   __shared__ uint32_t s_list[kSelThreads * kSelTilesPerWave];
   __shared__ uint32_t s_n;
   __shared__ unsigned long long s_base;
@@ -3370,7 +3376,7 @@ int rt_launch_adaptive_shard(rt_scene* sc, const rt_render_params* p, const doub
   if (n_tiles > 0) {
     hipLaunchKernelGGL(adaptive_select_kernel, dim3((unsigned)((n_tiles + kSelTilesPerBlock - 1) / kSelTilesPerBlock)),
                        dim3(kSelThreads), 0, st, d_primary,
-                       d_halo, d_out, p->out_format, G, threshold, tiles_x, n_tiles, list, cnt, 0u);
+                       d_halo, d_out, p->out_format, G, threshold, tiles_x, n_tiles, list, cnt, 0u, nullptr, nullptr);
     HIP_TRY(hipGetLastError());
   }
   rt_render_params q = *p;
@@ -3430,11 +3436,21 @@ int rt_launch_adaptive_frames(rt_scene* sc, const rt_render_params* p, int n_fra
   HIP_TRY(hipMemsetAsync(cnt, 0, sizeof(unsigned long long), st));
   const int tiles_x = (W + 7) / 8;
   const long long n_tiles = (long long)tiles_x * ((G.rows + 7) / 8);
-  for (int f = 0; f < n_frames && n_tiles > 0; ++f) {   // every frame's selection into one list
-    hipLaunchKernelGGL(adaptive_select_kernel, dim3((unsigned)((n_tiles + kSelTilesPerBlock - 1) / kSelTilesPerBlock)),
-                       dim3(kSelThreads), 0, st, d_primary[f],
-                       nullptr, d_out[f], p->out_format, G, threshold, tiles_x, n_tiles, list, cnt,
-                       (uint32_t)f << kListFrameShift);
+  // every frame's selection into one list, one launch (grid y = frame; the frame buffers'
+  // pointers travel in a small device table)
+  std::vector<const void*> ptrs(2 * (size_t)n_frames);
+  for (int f = 0; f < n_frames; ++f) {
+    ptrs[f] = d_primary[f];
+    ptrs[n_frames + f] = d_out[f];
+  }
+  void** d_ptrs = nullptr;
+  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&d_ptrs), ptrs.size() * sizeof(void*), st));
+  HIP_TRY(hipMemcpyAsync(d_ptrs, ptrs.data(), ptrs.size() * sizeof(void*), hipMemcpyHostToDevice, st));
+  if (n_tiles > 0) {
+    hipLaunchKernelGGL(adaptive_select_kernel,
+                       dim3((unsigned)((n_tiles + kSelTilesPerBlock - 1) / kSelTilesPerBlock), (unsigned)n_frames),
+                       dim3(kSelThreads), 0, st, nullptr, nullptr, nullptr, p->out_format, G, threshold, tiles_x,
+                       n_tiles, list, cnt, 0u, reinterpret_cast<const double* const*>(d_ptrs), d_ptrs + n_frames);
     HIP_TRY(hipGetLastError());
   }
   // every sample of every selected pixel of every frame in one launch: the sample buffer is sized
@@ -3460,6 +3476,7 @@ int rt_launch_adaptive_frames(rt_scene* sc, const rt_render_params* p, int n_fra
   (void)hipFreeAsync(list, st);
   (void)hipFreeAsync(cnt, st);
   (void)hipFreeAsync(samples, st);
+  (void)hipFreeAsync(d_ptrs, st);
   return rc;
 }
 
