@@ -336,8 +336,9 @@ def main():
             "frames_per_launch": frames_per_launch,
             "note": "achieved = HBM bytes per launch (rocprofv3 FETCH_SIZE/WRITE_SIZE of this workload, per frame, "
                     "x frames per launch; traffic) / mean launch duration (HIP events on the launch stream); "
-                    "frac = achieved / 8 TB/s.  The kernel is not HBM-bound: the scene is cache-resident and the "
-                    "binding resource is the CU's vector-L1 data path (l1_roof; DESIGN.md §5)",
+                    "frac = achieved / 8 TB/s.  The kernel is not HBM-bound: the scene is cache-resident; each wave "
+                    "is bound by its own dependent chain (node fetch, box test, stack pop) at 4 waves per SIMD "
+                    "(wave_cycles; l1_roof prices the vector-L1 data path; DESIGN.md §4-5)",
             # SURVEY §8d canonical work: 64 B per 2-wide node + 48 B per triangle test + 64 B per hit over
             # the reference median tree -- a measure of work, served from L1/L2, not HBM bytes
             "work_bytes_per_frame": int(work_bytes_frame),
@@ -349,6 +350,7 @@ def main():
                         "td_busy_frac": pmc.get("td_busy_frac") if pmc else None,
                         "def": "128*wide_node_visits + 80*tri_tests + 96*closest_hits (production kernel) / "
                                "(64 B/clk x 256 CUs x 2.4 GHz)"},
+            "wave_cycles": pmc_wave_mix(workload_key(a, n)),
         })
         out = {
             "metric": "Mrays/sec (primary+shadow+reflect), Office 1920x1080 1spp",
@@ -419,6 +421,28 @@ def pmc_per_frame(key):
             best = {"read": pf["hbm_read_bytes"], "write": pf["hbm_write_bytes"],
                     "td_busy_frac": d.get("_derived", {}).get("td_busy_frac"),
                     "source": str(path.relative_to(ROOT))}
+    return best
+
+
+def pmc_wave_mix(key):
+    """Where a wave's cycles go (rocprofv3 SQ counters of this workload, newest committed summary):
+    issuing an instruction, waiting on a memory counter, the rest (ready behind the SIMD's other
+    waves); None when no such pass was committed."""
+    best = None
+    for path in sorted(ROOT.glob("profiles/r*/pmc_*.json")):
+        try:
+            d = json.loads(path.read_text())
+        except (OSError, ValueError):
+            continue
+        if d.get("_workload") != key:
+            continue
+        try:
+            wc = d["SQ_WAVE_CYCLES"]["sum"]
+            issue, wait = d["SQ_ACTIVE_INST_ANY"]["sum"] / wc, d["SQ_WAIT_ANY"]["sum"] / wc
+        except (KeyError, TypeError, ZeroDivisionError):
+            continue
+        best = {"issue_frac": round(issue, 3), "mem_wait_frac": round(wait, 3),
+                "other_frac": round(1.0 - issue - wait, 3), "source": str(path.relative_to(ROOT))}
     return best
 
 
