@@ -3308,6 +3308,24 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
 }
 }  // namespace
 
+namespace {
+// stream-ordered scratch of one adaptive call, released on every return path (errors included)
+struct StreamScratch {
+  hipStream_t st;
+  std::vector<void*> ptrs;
+  template <typename T>
+  hipError_t alloc(T** out, size_t bytes) {
+    const hipError_t e = hipMallocAsync(reinterpret_cast<void**>(out), bytes, st);
+    if (e == hipSuccess) ptrs.push_back(*out);
+    return e;
+  }
+  ~StreamScratch() {
+    for (void* x : ptrs) (void)hipFreeAsync(x, st);
+  }
+};
+
+}  // namespace
+
 extern "C" {
 
 int rt_launch_compute_image(rt_scene* sc, const rt_render_params* p, void* d_out, rt_stats* stats, void* stream) {
@@ -3375,10 +3393,10 @@ int rt_launch_adaptive_shard(rt_scene* sc, const rt_render_params* p, const doub
   // interior pixels only can be selected
   const long long cap = (long long)std::max(0, W - 2) * G.rows;
   const int nsamp = subp * subp;
-  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&list), (size_t)std::max(1LL, cap) * sizeof(uint32_t), st));
-  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&cnt), sizeof(unsigned long long), st));
-  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&samples), (size_t)std::max(1LL, cap) * nsamp * 3 * sizeof(double),
-                         st));
+  StreamScratch scratch{st, {}};
+  HIP_TRY(scratch.alloc(&list, (size_t)std::max(1LL, cap) * sizeof(uint32_t)));
+  HIP_TRY(scratch.alloc(&cnt, sizeof(unsigned long long)));
+  HIP_TRY(scratch.alloc(&samples, (size_t)std::max(1LL, cap) * nsamp * 3 * sizeof(double)));
   HIP_TRY(hipMemsetAsync(cnt, 0, sizeof(unsigned long long), st));
   const int tiles_x = (W + 7) / 8;
   const long long n_tiles = (long long)tiles_x * ((G.rows + 7) / 8);
@@ -3402,9 +3420,6 @@ int rt_launch_adaptive_shard(rt_scene* sc, const rt_render_params* p, const doub
     HIP_TRY(hipStreamSynchronize(st));
     *n_selected = (long long)h;
   }
-  (void)hipFreeAsync(list, st);
-  (void)hipFreeAsync(cnt, st);
-  (void)hipFreeAsync(samples, st);
   return rc;
 }
 
@@ -3440,8 +3455,9 @@ int rt_launch_adaptive_frames(rt_scene* sc, const rt_render_params* p, int n_fra
   const long long cap = per * n_frames;
   uint32_t* list = nullptr;
   unsigned long long* cnt = nullptr;
-  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&list), (size_t)std::max(1LL, cap) * sizeof(uint32_t), st));
-  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&cnt), sizeof(unsigned long long), st));
+  StreamScratch scratch{st, {}};
+  HIP_TRY(scratch.alloc(&list, (size_t)std::max(1LL, cap) * sizeof(uint32_t)));
+  HIP_TRY(scratch.alloc(&cnt, sizeof(unsigned long long)));
   HIP_TRY(hipMemsetAsync(cnt, 0, sizeof(unsigned long long), st));
   const int tiles_x = (W + 7) / 8;
   const long long n_tiles = (long long)tiles_x * ((G.rows + 7) / 8);
@@ -3453,7 +3469,7 @@ int rt_launch_adaptive_frames(rt_scene* sc, const rt_render_params* p, int n_fra
     ptrs[n_frames + f] = d_out[f];
   }
   void** d_ptrs = nullptr;
-  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&d_ptrs), ptrs.size() * sizeof(void*), st));
+  HIP_TRY(scratch.alloc(&d_ptrs, ptrs.size() * sizeof(void*)));
   HIP_TRY(hipMemcpyAsync(d_ptrs, ptrs.data(), ptrs.size() * sizeof(void*), hipMemcpyHostToDevice, st));
   if (n_tiles > 0) {
     hipLaunchKernelGGL(adaptive_select_kernel,
@@ -3469,8 +3485,7 @@ int rt_launch_adaptive_frames(rt_scene* sc, const rt_render_params* p, int n_fra
   HIP_TRY(hipStreamSynchronize(st));
   const int nsamp = subp * subp;
   double* samples = nullptr;
-  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&samples),
-                         (size_t)std::max(1ull, n_sel) * nsamp * 3 * sizeof(double), st));
+  HIP_TRY(scratch.alloc(&samples, (size_t)std::max(1ull, n_sel) * nsamp * 3 * sizeof(double)));
   std::vector<rt_render_params> q(p, p + n_frames);
   for (auto& x : q) x.spp_n = subp;
   int rc = launch_render(sc, q.data(), n_frames, d_out, stats, stream, list, cnt, (long long)n_sel, samples);
@@ -3482,10 +3497,6 @@ int rt_launch_adaptive_frames(rt_scene* sc, const rt_render_params* p, int n_fra
     HIP_TRY(hipGetLastError());
   }
   if (n_selected) *n_selected = (long long)n_sel;
-  (void)hipFreeAsync(list, st);
-  (void)hipFreeAsync(cnt, st);
-  (void)hipFreeAsync(samples, st);
-  (void)hipFreeAsync(d_ptrs, st);
   return rc;
 }
 
