@@ -83,6 +83,9 @@ constexpr int kStackMask = kShortStack - 1;
 // of a launch run in fewer, fuller waves.  A handed-over lane's registers travel through the
 // donor thread's LDS stack entries (free between traversals): kMigWords words (packed; the
 // closest-hit distance and the hit attributes travel in the LDS slot, copied with it).
+#ifndef RT_BAND_ORDER   // several frames per launch: band-major work order
+#define RT_BAND_ORDER 1
+#endif
 #ifndef RT_DONATE_MAX
 #define RT_DONATE_MAX 24
 #endif
@@ -596,12 +599,24 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
             lrow = id != 0xffffffffu ? (int)(pix / (uint32_t)P.W) : P.rows;
             item = wk;
           } else {
+#if RT_BAND_ORDER
+            const long long tile = wk >> 6;
+            const int j = (int)(wk & 63);
+            // several frames: tile row ty of every frame, then row ty + 1, so each XCD head's
+            // contiguous range is a band of rows of all frames (its L2 holds one band's nodes)
+            const long long row_tiles = (long long)P.n_frames * P.tiles_x;
+            const long long ty = tile / row_tiles;
+            const long long rem = tile - ty * row_tiles;
+            frame = P.n_frames > 1 ? (int)(rem / P.tiles_x) : 0;
+            const int tx = (int)(rem - (long long)frame * P.tiles_x);
+#else
             long long tile = wk >> 6;
             const int j = (int)(wk & 63);
             frame = P.n_frames > 1 ? (int)(tile / P.frame_tiles) : 0;
             tile -= (long long)frame * P.frame_tiles;
             const long long ty = tile / P.tiles_x;
             const int tx = (int)(tile - ty * P.tiles_x);
+#endif
             px = tx * 8 + (j & 7);
             lrow = (int)ty * 8 + (j >> 3);
           }
