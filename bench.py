@@ -40,6 +40,7 @@ Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -78,9 +79,9 @@ def parse():
                     help="cpu_baseline threads (default: every CPU this process may run on, see usable_cpus)")
     ap.add_argument("--save", default="", help="rank 0: save the gathered image of the last frame (.npy)")
     ap.add_argument("--frames", type=int, default=0,
-                    help="frames per launch (rt_launch_frames, <= RT_MAX_FRAMES = 128, <= --steps; default 128): "
-                         "one persistent-kernel launch renders F consecutive frames from one work queue, so the "
-                         "per-launch drain is paid once per F")
+                    help="frames per launch (rt_launch_frames, <= RT_MAX_FRAMES = 128, <= --steps; default: "
+                         "default_frames(), 128 at 1 spp): one persistent-kernel launch renders F consecutive "
+                         "frames from one work queue, so the per-launch drain is paid once per F")
     ap.add_argument("--sweep", type=float, default=0.12,
                     help="animation path: frame f of a launch turns the camera by sweep*(f/(F-1) - 1/2) radians "
                          "about the image's vertical axis (rtamd.camera_orbit), so the batched frames are distinct "
@@ -150,7 +151,8 @@ def main():
     # one frame per launch (the halo exchange is per frame)
     batched_adaptive = a.adaptive and n == 1
     frame_bytes = rows_max * W * 3 * (4 + (8 if a.adaptive else 0))
-    F = 1 if (a.adaptive and not batched_adaptive) else max(1, min(a.frames or 128, rtamd.abi.RT_MAX_FRAMES, a.steps,
+    F = 1 if (a.adaptive and not batched_adaptive) else max(1, min(a.frames or default_frames(a), rtamd.abi.RT_MAX_FRAMES,
+                                                                   a.steps,
                                                                    int(a.frame_budget_gb * 1e9 // frame_bytes)))
     if n > 1 and not a.frames and not a.adaptive:
         # N > 1: at least two launches in the timed run, so the gather of one launch overlaps the
@@ -401,6 +403,17 @@ def main():
     if n > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def default_frames(a):
+    """Frames per launch when --frames is not given: about 2.6e8 samples per launch (a power of
+    two, 1..128).  One frame of many samples is already a long launch with a negligible drain,
+    and batching such frames costs coherence: a lane keeps its pixel through all n*n samples, and
+    with several frames per launch the waves' lanes drift apart (4K 4x4 spp: SIMD efficiency of
+    the node loop 0.88 at 1 frame, 0.76 at 16; 24.3 ms per frame at 2 frames per launch, 28.4 at
+    16; tools/batch_probe.py, tools/batch_diag.py).  At 1 spp more frames only help."""
+    samples = a.width * a.height * a.spp * a.spp
+    return int(min(128, max(1, 2 ** round(math.log2(max(1.0, 2.6e8 / samples))))))
 
 
 def pmc_per_frame(key):
