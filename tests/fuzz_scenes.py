@@ -114,3 +114,27 @@ def write_analytic(tmpdir, seed, width=64, height=48):
     with open(path, "a") as f:
         f.write("\n".join(lines) + "\n")
     return path
+
+
+def write_textured(tmpdir, seed, width=64, height=48):
+    """The seed's mesh scene plus a textured height field (OBJ vt coordinates, some outside [0, 1]
+    so the lookup clamps, mtllib / usemtl / map_Kd to a random P6 texture of odd size)."""
+    path = write(tmpdir, seed, width, height)
+    rng = random.Random(20_000 + seed)
+    r = lambda v: " ".join(repr(float(x)) for x in v)  # noqa: E731
+    nx, nz = rng.randint(1, 5), rng.randint(1, 5)
+    verts, tris = _strip(rng, nx, nz)
+    uv = [(rng.uniform(-0.2, 1.2), rng.uniform(-0.2, 1.2)) for _ in verts]
+    tw, th = rng.randint(1, 40), rng.randint(1, 30)
+    tex = bytes(rng.randrange(256) for _ in range(tw * th * 3))
+    (tmpdir / f"fuzz{seed}_tex.ppm").write_bytes(f"P6\n{tw} {th}\n255\n".encode() + tex)
+    (tmpdir / f"fuzz{seed}_tex.mtl").write_text(f"newmtl tex\nKd 1 1 1\nmap_Kd fuzz{seed}_tex.ppm\n")
+    obj = tmpdir / f"fuzz{seed}_tex.obj"
+    lines = [f"mtllib fuzz{seed}_tex.mtl"] + [f"v {r(v)}" for v in verts] + [f"vt {r(t)}" for t in uv]
+    lines += ["usemtl tex"] + ["f " + " ".join(f"{k + 1}/{k + 1}" for k in t) for t in tris]
+    obj.write_text("\n".join(lines) + "\n")
+    ka, kd, ks, shin, mirror, sh = _mat(rng)
+    mode = rng.choice(["FLAT", "PHONG"])
+    with open(path, "a") as f:
+        f.write(f"mesh {obj.name} {mode} {r(ka)} {r(kd)} {r(ks)} {float(shin)!r} {float(mirror)!r} {int(sh)}\n")
+    return path

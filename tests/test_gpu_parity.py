@@ -856,3 +856,19 @@ def test_fuzz_analytic_scene_matches_oracle(tmp_path, seed):
     assert np.abs(out.cpu().numpy() - want).max() <= TOL64
     assert counts(ast) == [acnt.primary_rays, acnt.shadow_rays, acnt.reflection_rays]
     dev.close()
+
+
+@pytest.mark.parametrize("seed", range(1, 40, 3))
+def test_fuzz_textured_scene_matches_oracle(tmp_path, seed):
+    # the random scenes plus a textured mesh (clamped uv lookups, odd texture sizes, FLAT / PHONG)
+    hs = rtamd.HostScene.load(fuzz_scenes.write_textured(tmp_path, seed, 64, 48))
+    hs.prepare()
+    orc = pyoracle.Oracle(hs.raw, hs)
+    p = hs.render_params(0, 0, 2 if seed % 2 else 1)
+    ref, cnt = orc.render(p, pyoracle.MODE_REFERENCE)
+    p.out_format = rtamd.RT_OUT_RGB_F64
+    dev = rtamd.DeviceScene(hs, 0)
+    img, st = dev.render(p)
+    assert np.abs(img - ref).max() <= TOL64
+    assert counts(st) == [cnt.primary_rays, cnt.shadow_rays, cnt.reflection_rays]
+    dev.close()
