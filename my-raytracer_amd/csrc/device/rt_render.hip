@@ -7,19 +7,29 @@
 //   -> lighting_device (+ diffuse_device, reflection_device)
 // with ONE kernel in which every lane runs a small state machine over the
 // rays of its pixel (primary -> per-light shadow rays -> reflection -> ...),
-// all ray kinds sharing one traversal loop:
-//   * traversal: ordered, t-culled, 2-wide fp32 nodes (rt_layout.hpp), the
-//     per-ray stack in LDS ([entry][thread], bank-conflict free), while-while
-//     loop; closest-hit for primary / reflection rays, any-hit bounded by the
+// all ray kinds sharing one traversal loop (DESIGN.md §4):
+//   * traversal: ordered, t-culled, speculative while-while over 4-wide fp32
+//     nodes (128 B, conservative outward-rounded boxes) of the device hierarchy
+//     (binned SAH with spatial splits by default); the top treelet is copied
+//     into each block's LDS; the per-ray stack is an LDS ring (8 entries, 16 on
+//     deep scenes: render_kernel<4, false, false, 16>) spilling to global
+//     memory; closest-hit for primary / reflection rays, any-hit bounded by the
 //     light distance for shadow rays (the reference traces full closest-hit
 //     shadow rays, mytracer_gpu.cu:653-660; the shadow predicate is the same);
+//     the closest hit is the smallest (t, reference slot), so any hierarchy
+//     over the same records gives the same bits;
 //   * triangle test and all shading in fp64 with the reference CPU
 //     renderer's operation order (mymesh.cpp:186-235, mytracer.cpp:510-608),
 //     compiled with fp-contract off, so hits are bit-identical to the oracle;
+//   * rays live in LDS slots (fp64 origin / direction / t-limit + 3 aux words
+//     holding the hit's barycentrics or the bounce normal); idle lanes are lent
+//     to owners for their extra shadow rays and reflection ray (fan-out);
 //   * work distribution: persistent workgroups pull 8x8 pixel tiles from 8
-//     work heads, one per XCD group (blockIdx % 8), refilled per wave with a
-//     single atomic when >= kRefill lanes are idle (__ballot + mbcnt), which
-//     keeps lanes busy despite divergent ray lengths;
+//     work heads on separate cache lines, one per XCD group, refilled per wave
+//     with a single atomic when >= kRefill lanes are idle; several frames per
+//     launch share the queue in band-major order (each head serves one row band
+//     of every frame); once the queue is empty, sparse waves hand their pixels
+//     to the other waves of their block (tail compaction);
 //   * reflection rays are spawned only when mirror > 0 (CPU semantics,
 //     mytracer.cpp:547); the reference GPU traces max_depth zero-weight
 //     bounces (mytracer_gpu.cu:281-310) — same pixels, less work.
