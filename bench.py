@@ -322,7 +322,7 @@ def main():
             single["rays_per_frame"] = int(rays_frame0)
             single["value"] = round(rays_frame0 / (single["ms_per_frame"] * 1e-3) / 1e6, 2)
             single["unit"] = "Mrays/s"
-        pmc = pmc_per_frame(workload_key(a, n))
+        pmc = pmc_per_frame(workload_key(a, n), frames_per_launch)
         kernel_s = kernel_ms_avg * 1e-3
         roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": None,
                 "traffic": None}
@@ -416,12 +416,14 @@ def default_frames(a):
     return int(min(128, max(1, 2 ** round(math.log2(max(1.0, 2.6e8 / samples))))))
 
 
-def pmc_per_frame(key):
+def pmc_per_frame(key, frames_per_launch=None):
     """HBM bytes per frame of this workload from the newest committed rocprofv3 --pmc summary
     (profiles/r*/pmc_*.json, tools/pmc_summary.py: production-kernel FETCH_SIZE / WRITE_SIZE summed
     over the profiled run's dispatches, divided by the frames they rendered, with the access-width
-    corrections of profiles/r*/hbm_calib.json), or None when this workload was not profiled."""
-    best = None
+    corrections of profiles/r*/hbm_calib.json), preferring one profiled at the same frames per
+    launch (fewer frames per launch read more per frame: the L2 starts cold each launch); None when
+    this workload was not profiled."""
+    best, best_same = None, None
     for path in sorted(ROOT.glob("profiles/r*/pmc_*.json")):
         try:
             d = json.loads(path.read_text())
@@ -434,7 +436,9 @@ def pmc_per_frame(key):
             best = {"read": pf["hbm_read_bytes"], "write": pf["hbm_write_bytes"],
                     "td_busy_frac": d.get("_derived", {}).get("td_busy_frac"),
                     "source": str(path.relative_to(ROOT))}
-    return best
+            if frames_per_launch is not None and d.get("_bench", {}).get("frames_per_launch") == frames_per_launch:
+                best_same = best
+    return best_same or best
 
 
 def pmc_wave_mix(key):
