@@ -94,3 +94,29 @@ def test_bench_two_ranks_rehearsal(tmp_path):
     ref, rays = expected_frames(320, 180, 8)
     assert np.array_equal(np.load(out), ref)
     assert d["config"]["rays_per_frame"] == rays
+
+
+def test_bench_four_ranks_driver_shape(tmp_path):
+    # the driver's command shape (--steps 20 --warmup 5, default frames per launch: 10 per rank
+    # launch, two launches in flight) with 4 ranks on this one GPU over gloo: stripes of 16 rows
+    # interleaved over 4 ranks, band-major frames inside each rank's launch; the assembled last
+    # frame equals the single-GPU render bit for bit
+    import os
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = tmp_path / "frame4.npy"
+    env = dict(os.environ, RT_BENCH_DEVICE="0")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), str(ROOT / "bench.py"),
+                        "--gpus", "4", "--dist-backend", "gloo", "--steps", "20", "--warmup", "5",
+                        "--width", "320", "--height", "180", "--no-cpu-baseline", "--save", str(out)],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["n_gpus"] == 4 and d["config"]["frames_per_launch"] == 10 and d["steps"] == 20
+    ref, rays = expected_frames(320, 180, 10)
+    assert np.array_equal(np.load(out), ref)
+    assert d["config"]["rays_per_frame"] == rays
