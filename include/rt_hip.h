@@ -162,13 +162,41 @@ int rt_scene_upload(const rt_scene_soa* soa, const rt_bvh_soa* bvh, int device, 
  *   RT_TREE_SAH        binned-SAH tree over all triangles (object splits only), 4-wide collapsed
  *   RT_TREE_REFERENCE  the reference median-split tree, oversize leaves refined */
 enum { RT_TREE_SAH = 0, RT_TREE_REFERENCE = 1, RT_TREE_SBVH = 2 };
+/* 4-wide collapse of the device hierarchy: open the child with the largest box (default), or
+ * the SAH-optimal choice of up to 4 slots per node (dynamic programme). */
+enum { RT_COLLAPSE_GREEDY = 0, RT_COLLAPSE_SAH = 1 };
+
+/* Upload options.  The library reads nothing from the environment: its behaviour depends only
+ * on these fields and the call's arguments.  Fill with rt_upload_options_init (the defaults),
+ * then change fields.  None of them changes a pixel or a ray count: they pick
+ * the device hierarchy, its build, and the kernel's LDS / grid layout. */
 typedef struct rt_upload_options {
-  int device_tree;      /* RT_TREE_* */
-  int reserved_[7];
+  int device_tree;       /* RT_TREE_* (default RT_TREE_SBVH) */
+  int build_threads;     /* host threads of the builders; 0 = the hardware threads, at most 64.
+                            The hierarchy does not depend on it */
+  int stack_ring;        /* LDS stack-ring entries of the production kernel: 0 = by size (16 from 2^18
+                            device records on, else 8; default), 8 or 16 */
+  int lds_treelet;       /* 4-wide nodes each block caches in LDS: < 0 = as many as fit (default),
+                            else at most this many */
+  int collapse;          /* RT_COLLAPSE_* (default RT_COLLAPSE_GREEDY) */
+  int sbvh_leaf_max;     /* SBVH: SAH-terminated leaves of up to this many references (default 2;
+                            1 = split down to single references), 1..8 */
+  int sbvh_bins;         /* SBVH: spatial bins per axis (default 32), 2..128 */
+  int blocks_per_cu;     /* persistent blocks per CU: 0 = as many as fit (default), else at most this many */
+  int grid_spare;        /* block slots of the persistent grid left free for concurrent kernels (default 0) */
+  int verbose;           /* 1: build phase times to stderr (default 0) */
+  double sbvh_alpha;     /* SBVH: try spatial splits where the best object split's children overlap by
+                            more than alpha x the root's surface area (default 1e-5) */
+  double sbvh_budget;    /* SBVH: at most this many extra references per triangle (default 0.75) */
+  double sbvh_c_trav;    /* SBVH: node visit cost in triangle tests, for leaf termination (default 1.0) */
+  double collapse_c_tri; /* RT_COLLAPSE_SAH: cost of a leaf slot per unit area (default 1.0) */
+  int reserved_[8];
 } rt_upload_options;
 
-/* rt_scene_upload with options (NULL = defaults; the environment variable
- * RT_DEVICE_TREE=reference|sah|sbvh changes the default for A/B runs). */
+/* Fills *opt with the defaults listed above. */
+void rt_upload_options_init(rt_upload_options* opt);
+
+/* rt_scene_upload with options (NULL = defaults). */
 int rt_scene_upload_ex(const rt_scene_soa* soa, const rt_bvh_soa* bvh, int device, const rt_upload_options* opt,
                        rt_scene** out);
 

@@ -34,7 +34,7 @@ int rt_multi_create(const rt_scene_soa* soa, const rt_bvh_soa* bvh, const int* d
 /* Number of GPUs of the driver. */
 int rt_multi_device_count(const rt_multi* m);
 
-/* Renders one whole frame (p->row_begin / row_end / stripe_* are ignored: every row is
+/* Renders one whole frame (rt_multi_render_frames with one frame; p->row_begin / row_end / stripe_* are ignored: every row is
  * rendered, sharded as above with the given stripe_height >= 1) into d_out, a DEVICE
  * buffer on devices[0] holding height x width x 3 values of p->out_format, row-major,
  * row 0 first (the layout of rt_launch_compute_image).  Synchronous.  stats (optional):
@@ -42,6 +42,20 @@ int rt_multi_device_count(const rt_multi* m);
  * the assembled frame (render + gather + re-interleave). */
 int rt_multi_render(rt_multi* m, const rt_render_params* p, int stripe_height, void* d_out, rt_stats* stats,
                     double* ms);
+
+/* Renders n_frames whole frames: frame f renders p[f] into d_outs[f] (device buffers on
+ * devices[0], layout as rt_multi_render); the frames must share size and out_format (they may
+ * differ as rt_launch_frames allows: camera vectors).  Frames go in batches of up to
+ * RT_MAX_FRAMES: every GPU renders its stripes of a batch in ONE rt_launch_frames (the
+ * per-launch drain is paid once per batch), one ncclGather per batch collects the stripe blocks
+ * on devices[0], and one kernel re-interleaves every frame of the batch.  Two batches are in
+ * flight on separate streams and communicators (double-buffered stripe buffers), so the gather
+ * and re-interleave of batch i proceed while batch i + 1 renders (at least two batches when
+ * n_frames >= 2).  Synchronous; results equal n_frames rt_multi_render calls.  stats / ms as
+ * rt_multi_render (stats synchronises every launch, so pass NULL when timing).  Replaces the
+ * reference's single-device launch_compute_image_device (mytracer_gpu.cu:32-113) for a node. */
+int rt_multi_render_frames(rt_multi* m, const rt_render_params* p, int n_frames, int stripe_height,
+                           void* const* d_outs, rt_stats* stats, double* ms);
 
 /* rt_multi_render into a HOST buffer (the frame is copied from devices[0] after ms is taken). */
 int rt_multi_render_to_host(rt_multi* m, const rt_render_params* p, int stripe_height, void* host_out,
@@ -56,6 +70,12 @@ int rt_multi_max_rows(int height, int stripe_height, int n);
  * frame.  Same index map as the device kernel. */
 int rt_multi_interleave_host(const void* gathered, void* out, int height, int width, int channels, int elem_bytes,
                              int stripe_height, int n);
+
+/* The same for a batch: gathered holds n blocks of n_frames x max_rows x width x channels
+ * elements (GPU g's stripes of every frame of the batch, as rt_multi_render_frames gathers them);
+ * outs[f] receives frame f. */
+int rt_multi_interleave_frames_host(const void* gathered, void* const* outs, int n_frames, int height, int width,
+                                    int channels, int elem_bytes, int stripe_height, int n);
 
 void rt_multi_free(rt_multi* m);
 

@@ -1,5 +1,8 @@
 // rt_multi.hip — single-process multi-GPU driver (include/rt_multi.h): row stripes per GPU,
 // one RCCL gather to devices[0], a re-interleave kernel there.  SURVEY §8(e).
+// Frames go in batches (one rt_launch_frames per GPU per batch, so the per-launch drain is paid
+// once per batch), and two batches are in flight: batch i + 1 renders on the other slot's
+// streams while batch i's gather and re-interleave drain.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -52,18 +55,47 @@ int max_rows_of(int h, int sh, int n) {
 }
 
 // One thread per 4-B word of an output row (rows are width x 3 x 4 or 8 bytes, so 4-B
-// aligned): row y of the frame comes from its shard's packed buffer in the gathered array
-// [n][max_rows][row_bytes].
-__global__ void interleave_kernel(const uint32_t* __restrict__ gathered, uint32_t* __restrict__ out, int height,
-                                  size_t row_words, int sh, int n, int max_rows) {
-  const int y = blockIdx.y;
+// aligned): row y of frame f = blockIdx.z comes from its shard's packed buffer in the gathered
+// array [n][n_frames][max_rows][row_bytes] (each GPU sends its frames' stripes as one block).
+__global__ void interleave_kernel(const uint32_t* __restrict__ gathered, uint32_t* const* __restrict__ outs,
+                                  int n_frames, size_t row_words, int sh, int n, int max_rows) {
+  const int y = blockIdx.y, f = blockIdx.z;
   int shard, lrow;
   stripe_source(y, sh, n, shard, lrow);
-  const uint32_t* src = gathered + ((size_t)shard * max_rows + lrow) * row_words;
-  uint32_t* dst = out + (size_t)y * row_words;
+  const uint32_t* src = gathered + (((size_t)shard * n_frames + f) * max_rows + lrow) * row_words;
+  uint32_t* dst = outs[f] + (size_t)y * row_words;
   for (size_t c = blockIdx.x * (size_t)blockDim.x + threadIdx.x; c < row_words; c += (size_t)gridDim.x * blockDim.x)
     dst[c] = src[c];
 }
+
+void interleave_host(const void* gathered, void* const* outs, int n_frames, int height, size_t row_bytes, int sh,
+                     int n) {
+  const int mr = max_rows_of(height, sh, n);
+  for (int f = 0; f < n_frames; ++f)
+    for (int y = 0; y < height; ++y) {
+      int shard, lrow;
+      stripe_source(y, sh, n, shard, lrow);
+      std::memcpy(static_cast<unsigned char*>(outs[f]) + (size_t)y * row_bytes,
+                  static_cast<const unsigned char*>(gathered) + (((size_t)shard * n_frames + f) * mr + lrow) * row_bytes,
+                  row_bytes);
+    }
+}
+
+// A batch in flight: per device its stripe buffers for the batch's frames and the streams its
+// launch and gather run on, on devices[0] the gathered array and the output table.  Two slots
+// alternate, each with its own communicators, so the collectives of two batches never share a
+// communicator across streams.
+constexpr int kSlots = 2;
+struct Slot {
+  std::vector<ncclComm_t> comms;
+  std::vector<hipStream_t> streams;
+  std::vector<void*> sbuf;       // per device: [frames][max_rows][row_bytes]
+  void* gbuf = nullptr;          // devices[0]: [n][frames][max_rows][row_bytes]
+  void** d_outs = nullptr;       // devices[0]: [RT_MAX_FRAMES] output pointers of the batch
+  void** h_outs = nullptr;       // pinned staging of the same
+  hipEvent_t done = nullptr;     // devices[0]: the batch's re-interleave finished
+  bool busy = false;
+};
 
 }  // namespace
 
@@ -71,12 +103,8 @@ struct rt_multi {
   int n = 0;
   std::vector<int> devices;
   std::vector<rt_scene*> scenes;
-  std::vector<ncclComm_t> comms;
-  std::vector<hipStream_t> streams;
-  std::vector<void*> sbuf;     // per device: its packed stripes (max_rows x row_bytes)
-  size_t sbuf_bytes = 0;
-  void* gbuf = nullptr;        // devices[0]: n x max_rows x row_bytes
-  size_t gbuf_bytes = 0;
+  Slot slot[kSlots];
+  size_t sbuf_bytes = 0;       // bytes of every slot's per-device stripe buffer
 };
 
 extern "C" {
@@ -90,17 +118,17 @@ int rt_multi_max_rows(int height, int stripe_height, int n) {
 
 int rt_multi_interleave_host(const void* gathered, void* out, int height, int width, int channels, int elem_bytes,
                              int stripe_height, int n) {
-  if (!gathered || !out || height <= 0 || width <= 0 || channels <= 0 || elem_bytes <= 0 || stripe_height < 1 ||
-      n < 1)
+  return rt_multi_interleave_frames_host(gathered, &out, 1, height, width, channels, elem_bytes, stripe_height, n);
+}
+
+int rt_multi_interleave_frames_host(const void* gathered, void* const* outs, int n_frames, int height, int width,
+                                    int channels, int elem_bytes, int stripe_height, int n) {
+  if (!gathered || !outs || n_frames < 1 || height <= 0 || width <= 0 || channels <= 0 || elem_bytes <= 0 ||
+      stripe_height < 1 || n < 1)
     return fail(RT_ERR_INVALID, "rt_multi_interleave_host: bad argument");
-  const int mr = max_rows_of(height, stripe_height, n);
-  const size_t row_bytes = (size_t)width * channels * elem_bytes;
-  for (int y = 0; y < height; ++y) {
-    int shard, lrow;
-    stripe_source(y, stripe_height, n, shard, lrow);
-    std::memcpy(static_cast<unsigned char*>(out) + (size_t)y * row_bytes,
-                static_cast<const unsigned char*>(gathered) + ((size_t)shard * mr + lrow) * row_bytes, row_bytes);
-  }
+  for (int f = 0; f < n_frames; ++f)
+    if (!outs[f]) return fail(RT_ERR_INVALID, "rt_multi_interleave_host: null output frame");
+  interleave_host(gathered, outs, n_frames, height, (size_t)width * channels * elem_bytes, stripe_height, n);
   return RT_OK;
 }
 
@@ -109,14 +137,21 @@ void rt_multi_free(rt_multi* m) {
   for (int g = 0; g < (int)m->devices.size(); ++g) {
     (void)hipSetDevice(m->devices[g]);
     (void)hipDeviceSynchronize();
-    if (g < (int)m->sbuf.size() && m->sbuf[g]) (void)hipFree(m->sbuf[g]);
-    if (g < (int)m->streams.size() && m->streams[g]) (void)hipStreamDestroy(m->streams[g]);
-    if (g < (int)m->comms.size() && m->comms[g]) (void)ncclCommDestroy(m->comms[g]);
+    for (Slot& S : m->slot) {
+      if (g < (int)S.sbuf.size() && S.sbuf[g]) (void)hipFree(S.sbuf[g]);
+      if (g < (int)S.streams.size() && S.streams[g]) (void)hipStreamDestroy(S.streams[g]);
+      if (g < (int)S.comms.size() && S.comms[g]) (void)ncclCommDestroy(S.comms[g]);
+    }
     if (g < (int)m->scenes.size()) rt_scene_free(m->scenes[g]);
   }
-  if (m->gbuf) {
+  if (!m->devices.empty()) {
     (void)hipSetDevice(m->devices[0]);
-    (void)hipFree(m->gbuf);
+    for (Slot& S : m->slot) {
+      if (S.gbuf) (void)hipFree(S.gbuf);
+      if (S.d_outs) (void)hipFree(S.d_outs);
+      if (S.h_outs) (void)hipHostFree(S.h_outs);
+      if (S.done) (void)hipEventDestroy(S.done);
+    }
   }
   delete m;
 }
@@ -137,21 +172,31 @@ int rt_multi_create(const rt_scene_soa* soa, const rt_bvh_soa* bvh, const int* d
     rt_multi_free(m);
     return fail(RT_ERR_HIP, "rt_multi_create: " + e);
   }
-  m->comms.assign(n_devices, nullptr);
-  m->streams.assign(n_devices, nullptr);
-  m->sbuf.assign(n_devices, nullptr);
-  for (int g = 0; g < n_devices; ++g) {
-    if (hipSetDevice(devices[g]) != hipSuccess ||
-        hipStreamCreateWithFlags(&m->streams[g], hipStreamNonBlocking) != hipSuccess) {
-      rt_multi_free(m);
-      return fail(RT_ERR_HIP, "rt_multi_create: stream creation failed");
+  for (Slot& S : m->slot) {
+    S.comms.assign(n_devices, nullptr);
+    S.streams.assign(n_devices, nullptr);
+    S.sbuf.assign(n_devices, nullptr);
+    for (int g = 0; g < n_devices; ++g) {
+      if (hipSetDevice(devices[g]) != hipSuccess ||
+          hipStreamCreateWithFlags(&S.streams[g], hipStreamNonBlocking) != hipSuccess) {
+        rt_multi_free(m);
+        return fail(RT_ERR_HIP, "rt_multi_create: stream creation failed");
+      }
     }
-  }
-  const ncclResult_t r = ncclCommInitAll(m->comms.data(), n_devices, devices);
-  if (r != ncclSuccess) {
-    m->comms.assign(n_devices, nullptr);
-    rt_multi_free(m);
-    return fail(RT_ERR_HIP, std::string("rt_multi_create: ncclCommInitAll: ") + ncclGetErrorString(r));
+    if (hipSetDevice(devices[0]) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&S.d_outs), RT_MAX_FRAMES * sizeof(void*)) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void**>(&S.h_outs), RT_MAX_FRAMES * sizeof(void*), hipHostMallocDefault) !=
+            hipSuccess ||
+        hipEventCreateWithFlags(&S.done, hipEventDisableTiming) != hipSuccess) {
+      rt_multi_free(m);
+      return fail(RT_ERR_HIP, "rt_multi_create: output table allocation failed");
+    }
+    const ncclResult_t r = ncclCommInitAll(S.comms.data(), n_devices, devices);
+    if (r != ncclSuccess) {
+      S.comms.assign(n_devices, nullptr);
+      rt_multi_free(m);
+      return fail(RT_ERR_HIP, std::string("rt_multi_create: ncclCommInitAll: ") + ncclGetErrorString(r));
+    }
   }
   *out = m;
   return RT_OK;
@@ -159,78 +204,121 @@ int rt_multi_create(const rt_scene_soa* soa, const rt_bvh_soa* bvh, const int* d
 
 int rt_multi_device_count(const rt_multi* m) { return m ? m->n : 0; }
 
-int rt_multi_render(rt_multi* m, const rt_render_params* p, int stripe_height, void* d_out, rt_stats* stats,
-                    double* ms) {
-  if (!m || !p || !d_out || stripe_height < 1) return fail(RT_ERR_INVALID, "rt_multi_render: bad argument");
+// Largest batch: frames per launch bounded by RT_MAX_FRAMES and by the gathered array on
+// devices[0] (n x frames x shard bytes per slot, at most 8 GB of its 288 GB).
+static int batch_cap(int n, size_t shard_bytes) {
+  const size_t budget = (size_t)8 << 30;
+  const size_t per_frame = std::max<size_t>(1, shard_bytes * (size_t)n);
+  return (int)std::max<size_t>(1, std::min<size_t>(RT_MAX_FRAMES, budget / per_frame));
+}
+
+int rt_multi_render_frames(rt_multi* m, const rt_render_params* p, int n_frames, int stripe_height,
+                           void* const* d_outs, rt_stats* stats, double* ms) {
+  if (!m || !p || !d_outs || stripe_height < 1 || n_frames < 1)
+    return fail(RT_ERR_INVALID, "rt_multi_render_frames: bad argument");
   if (p->out_format != RT_OUT_RGB_F32 && p->out_format != RT_OUT_RGB_F64)
-    return fail(RT_ERR_INVALID, "rt_multi_render: bad out_format");
+    return fail(RT_ERR_INVALID, "rt_multi_render_frames: bad out_format");
   const int n = m->n, W = p->camera.width, H = p->camera.height;
-  if (W <= 0 || H <= 0) return fail(RT_ERR_INVALID, "rt_multi_render: bad image size");
+  if (W <= 0 || H <= 0) return fail(RT_ERR_INVALID, "rt_multi_render_frames: bad image size");
+  for (int f = 0; f < n_frames; ++f) {
+    if (!d_outs[f]) return fail(RT_ERR_INVALID, "rt_multi_render_frames: null output buffer");
+    if (p[f].camera.width != W || p[f].camera.height != H || p[f].out_format != p->out_format)
+      return fail(RT_ERR_INVALID, "rt_multi_render_frames: frames must share size and format");
+  }
   const int elem = p->out_format == RT_OUT_RGB_F64 ? 8 : 4;
   const int mr = max_rows_of(H, stripe_height, n);
   const size_t row_bytes = (size_t)W * 3 * elem;
   const size_t shard_bytes = (size_t)mr * row_bytes;
-  if (shard_bytes > m->sbuf_bytes) {   // (re)allocate the stripe buffers for this frame size
+  const int cap = batch_cap(n, shard_bytes);
+  // at least two batches when there are two frames, so a gather overlaps the next launch
+  const int n_batches = std::max((n_frames + cap - 1) / cap, std::min(n_frames, kSlots));
+  const int per = (n_frames + n_batches - 1) / n_batches;
+  const size_t need = shard_bytes * (size_t)per;
+  if (need > m->sbuf_bytes) {   // (re)allocate every slot's buffers for this batch size
+    for (Slot& S : m->slot) {
+      for (int g = 0; g < n; ++g) {
+        HIP_TRY(hipSetDevice(m->devices[g]));
+        HIP_TRY(hipDeviceSynchronize());
+        if (S.sbuf[g]) HIP_TRY(hipFree(S.sbuf[g]));
+        S.sbuf[g] = nullptr;
+        HIP_TRY(hipMalloc(&S.sbuf[g], need));
+      }
+      HIP_TRY(hipSetDevice(m->devices[0]));
+      if (S.gbuf) HIP_TRY(hipFree(S.gbuf));
+      S.gbuf = nullptr;
+      HIP_TRY(hipMalloc(&S.gbuf, need * n));
+      S.busy = false;
+    }
+    m->sbuf_bytes = need;
+  }
+  if (stats) std::memset(stats, 0, sizeof *stats);
+  const auto t0 = std::chrono::steady_clock::now();
+  std::vector<rt_render_params> q((size_t)per);
+  std::vector<void*> outs((size_t)per);
+  for (int b = 0, f0 = 0; f0 < n_frames; ++b, f0 += per) {
+    const int F = std::min(per, n_frames - f0);
+    Slot& S = m->slot[b % kSlots];
+    if (S.busy) {   // batch b - 2 re-interleaved: its buffers and pinned output table are free again
+      HIP_TRY(hipSetDevice(m->devices[0]));
+      HIP_TRY(hipEventSynchronize(S.done));
+    }
+    // every GPU renders its stripes of the batch's frames in one launch on the slot's stream
+    for (int g = 0; g < n; ++g) {
+      for (int f = 0; f < F; ++f) {
+        q[f] = p[f0 + f];
+        q[f].row_begin = 0;
+        q[f].row_end = H;
+        q[f].stripe_height = stripe_height;
+        q[f].stripe_count = n;
+        q[f].stripe_index = g;
+        outs[f] = static_cast<unsigned char*>(S.sbuf[g]) + (size_t)f * shard_bytes;
+      }
+      rt_stats st;
+      if (rt_launch_frames(m->scenes[g], q.data(), F, outs.data(), stats ? &st : nullptr, S.streams[g]) != RT_OK)
+        return fail(RT_ERR_HIP, std::string("rt_multi_render_frames: device ") + std::to_string(m->devices[g]) +
+                                    ": " + rt_last_error());
+      if (stats) {
+        stats->primary_rays += st.primary_rays;
+        stats->shadow_rays += st.shadow_rays;
+        stats->reflection_rays += st.reflection_rays;
+        stats->pixels += st.pixels;
+      }
+    }
+    // ONE gather of the batch's padded stripe blocks to devices[0] (each rank sends on its own link)
+    const size_t count = shard_bytes * (size_t)F / elem;
+    const ncclDataType_t type = elem == 8 ? ncclFloat64 : ncclFloat32;
+    NCCL_TRY(ncclGroupStart());
+    for (int g = 0; g < n; ++g)
+      NCCL_TRY(ncclGather(S.sbuf[g], g == 0 ? S.gbuf : nullptr, count, type, 0, S.comms[g], S.streams[g]));
+    NCCL_TRY(ncclGroupEnd());
+    // re-interleave the stripes into the batch's frames on devices[0]
+    HIP_TRY(hipSetDevice(m->devices[0]));
+    for (int f = 0; f < F; ++f) S.h_outs[f] = d_outs[f0 + f];
+    HIP_TRY(hipMemcpyAsync(S.d_outs, S.h_outs, (size_t)F * sizeof(void*), hipMemcpyHostToDevice, S.streams[0]));
+    const size_t row_words = row_bytes / 4;
+    const unsigned bx = (unsigned)std::min<size_t>((row_words + 255) / 256, 64);
+    interleave_kernel<<<dim3(bx, (unsigned)H, (unsigned)F), dim3(256), 0, S.streams[0]>>>(
+        static_cast<const uint32_t*>(S.gbuf), reinterpret_cast<uint32_t* const*>(S.d_outs), F, row_words,
+        stripe_height, n, mr);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(S.done, S.streams[0]));
+    S.busy = true;
+  }
+  for (Slot& S : m->slot)
     for (int g = 0; g < n; ++g) {
       HIP_TRY(hipSetDevice(m->devices[g]));
-      HIP_TRY(hipDeviceSynchronize());
-      if (m->sbuf[g]) HIP_TRY(hipFree(m->sbuf[g]));
-      m->sbuf[g] = nullptr;
-      HIP_TRY(hipMalloc(&m->sbuf[g], shard_bytes));
+      HIP_TRY(hipStreamSynchronize(S.streams[g]));
     }
-    m->sbuf_bytes = shard_bytes;
-    HIP_TRY(hipSetDevice(m->devices[0]));
-    if (m->gbuf) HIP_TRY(hipFree(m->gbuf));
-    m->gbuf = nullptr;
-    HIP_TRY(hipMalloc(&m->gbuf, shard_bytes * n));
-    m->gbuf_bytes = shard_bytes * n;
-  }
-  const auto t0 = std::chrono::steady_clock::now();
-  // every GPU renders its stripes (asynchronous launches on its own stream)
-  for (int g = 0; g < n; ++g) {
-    rt_render_params q = *p;
-    q.row_begin = 0;
-    q.row_end = H;
-    q.stripe_height = stripe_height;
-    q.stripe_count = n;
-    q.stripe_index = g;
-    if (rt_launch_compute_image(m->scenes[g], &q, m->sbuf[g], nullptr, m->streams[g]) != RT_OK)
-      return fail(RT_ERR_HIP, std::string("rt_multi_render: device ") + std::to_string(m->devices[g]) + ": " +
-                                  rt_last_error());
-  }
-  // ONE gather of the padded stripe buffers to devices[0] (each rank sends on its own link)
-  const size_t count = shard_bytes / elem;
-  const ncclDataType_t type = elem == 8 ? ncclFloat64 : ncclFloat32;
-  NCCL_TRY(ncclGroupStart());
-  for (int g = 0; g < n; ++g)
-    NCCL_TRY(ncclGather(m->sbuf[g], g == 0 ? m->gbuf : nullptr, count, type, 0, m->comms[g], m->streams[g]));
-  NCCL_TRY(ncclGroupEnd());
-  // re-interleave the stripes into the frame on devices[0]
-  HIP_TRY(hipSetDevice(m->devices[0]));
-  const size_t row_words = row_bytes / 4;
-  const unsigned bx = (unsigned)std::min<size_t>((row_words + 255) / 256, 64);
-  interleave_kernel<<<dim3(bx, (unsigned)H), dim3(256), 0, m->streams[0]>>>(
-      static_cast<const uint32_t*>(m->gbuf), static_cast<uint32_t*>(d_out), H, row_words, stripe_height, n, mr);
-  HIP_TRY(hipGetLastError());
-  for (int g = 0; g < n; ++g) {
-    HIP_TRY(hipSetDevice(m->devices[g]));
-    HIP_TRY(hipStreamSynchronize(m->streams[g]));
-  }
+  for (Slot& S : m->slot) S.busy = false;
   const double t = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (ms) *ms = t;
-  if (stats) {   // raw counter words [8, 11) of each GPU's launch = primary / shadow / reflection rays
-    std::memset(stats, 0, sizeof *stats);
-    for (int g = 0; g < n; ++g) {
-      unsigned long long w[32] = {};
-      if (rt_debug_counters(m->scenes[g], w, 32) < 32) return fail(RT_ERR_HIP, "rt_multi_render: counters");
-      if (w[31] != 0) return fail(RT_ERR_HIP, "rt_multi_render: persistent-loop watchdog fired (kernel bug)");
-      stats->primary_rays += (long long)w[8];
-      stats->shadow_rays += (long long)w[9];
-      stats->reflection_rays += (long long)w[10];
-      stats->pixels += (long long)w[14];
-    }
-  }
   return RT_OK;
+}
+
+int rt_multi_render(rt_multi* m, const rt_render_params* p, int stripe_height, void* d_out, rt_stats* stats,
+                    double* ms) {
+  if (!d_out) return fail(RT_ERR_INVALID, "rt_multi_render: bad argument");
+  return rt_multi_render_frames(m, p, 1, stripe_height, &d_out, stats, ms);
 }
 
 int rt_multi_render_to_host(rt_multi* m, const rt_render_params* p, int stripe_height, void* host_out,

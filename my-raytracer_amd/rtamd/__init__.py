@@ -83,6 +83,41 @@ def _check_hip(rc, what):
         raise RtError(f"{what}: {hip_lib().rt_last_error().decode()}")
 
 
+def usable_cpus():
+    """CPUs this process may run on: the affinity mask, bounded by a cgroup CPU quota (the GPU
+    box grants 16 CPUs of a 256-thread host per GPU)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+_TREES = {"sah": abi.RT_TREE_SAH, "reference": abi.RT_TREE_REFERENCE, "sbvh": abi.RT_TREE_SBVH}
+
+
+def upload_options(tree=None, **fields):
+    """rt_upload_options with the library defaults (rt_upload_options_init), the device tree
+    (None = default, or "sbvh" / "sah" / "reference") and any other fields set.  build_threads
+    defaults to usable_cpus() (the library would use every hardware thread)."""
+    opt = abi.UploadOptions()
+    hip_lib().rt_upload_options_init(C.byref(opt))
+    opt.build_threads = usable_cpus()
+    if tree is not None:
+        if tree not in _TREES:
+            raise ValueError(f"tree must be one of {sorted(_TREES)}")
+        opt.device_tree = _TREES[tree]
+    names = {n for n, _ in abi.UploadOptions._fields_ if n != "reserved_"}
+    for k, v in fields.items():
+        if k not in names:
+            raise ValueError(f"unknown upload option {k!r}")
+        setattr(opt, k, v)
+    return opt
+
+
 def _np(ptr, count, dtype):
     if count == 0:
         return np.zeros(0, dtype=dtype)
@@ -198,23 +233,18 @@ class HostScene:
 class DeviceScene:
     """Scene resident on one MI355X (rt_scene*), uploaded from a prepared HostScene."""
 
-    def __init__(self, host_scene, device=0, analytic=False, tree=None):
+    def __init__(self, host_scene, device=0, analytic=False, tree=None, **options):
         """analytic=True also uploads the raw scene's spheres and planes (rt_scene_set_analytic,
         CPU intersect_scene semantics); the default traces meshes only, like the reference GPU
         path (mytracer_gpu.cu:314-328).  tree: None (library default, "sbvh": SAH with
-        spatial splits), "sbvh", "sah" (object splits only) or "reference" -- the device traversal hierarchy (pixels and ray counts do not depend on it)."""
+        spatial splits), "sbvh", "sah" (object splits only) or "reference" -- the device
+        traversal hierarchy (pixels and ray counts do not depend on it).  options: other
+        rt_upload_options fields (stack_ring=16, lds_treelet=0, sbvh_leaf_max=1, ...)."""
         self._h = C.c_void_p()
         self.device = device
-        if tree is None:
-            _check_hip(hip_lib().rt_scene_upload(host_scene.soa, host_scene.bvh, device, C.byref(self._h)),
-                       "rt_scene_upload")
-        else:
-            kinds = {"sah": abi.RT_TREE_SAH, "reference": abi.RT_TREE_REFERENCE, "sbvh": abi.RT_TREE_SBVH}
-            if tree not in kinds:
-                raise ValueError(f"tree must be one of {sorted(kinds)}")
-            opt = abi.UploadOptions(device_tree=kinds[tree])
-            _check_hip(hip_lib().rt_scene_upload_ex(host_scene.soa, host_scene.bvh, device, C.byref(opt),
-                                                    C.byref(self._h)), "rt_scene_upload_ex")
+        opt = upload_options(tree, **options)
+        _check_hip(hip_lib().rt_scene_upload_ex(host_scene.soa, host_scene.bvh, device, C.byref(opt),
+                                                C.byref(self._h)), "rt_scene_upload_ex")
         self.tree = tree
         self.analytic = False
         if analytic:
@@ -421,14 +451,12 @@ class MultiScene:
     """One scene on several GPUs of this node, one process (rt_multi.h): every frame is cut
     into interleaved row stripes per GPU and assembled on devices[0] by one RCCL gather."""
 
-    def __init__(self, host_scene, devices=(0,), tree=None):
+    def __init__(self, host_scene, devices=(0,), tree=None, **options):
         self._h = C.c_void_p()
         devs = (C.c_int * len(devices))(*devices)
-        opt = None
-        if tree is not None:
-            kinds = {"sah": abi.RT_TREE_SAH, "reference": abi.RT_TREE_REFERENCE, "sbvh": abi.RT_TREE_SBVH}
-            opt = C.byref(abi.UploadOptions(device_tree=kinds[tree]))
-        rc = multi_lib().rt_multi_create(host_scene.soa, host_scene.bvh, devs, len(devices), opt, C.byref(self._h))
+        opt = upload_options(tree, **options)
+        rc = multi_lib().rt_multi_create(host_scene.soa, host_scene.bvh, devs, len(devices), C.byref(opt),
+                                         C.byref(self._h))
         if rc != RT_OK:
             raise RtError(f"rt_multi_create: {multi_lib().rt_multi_last_error().decode()}")
         self.devices = tuple(devices)
@@ -444,6 +472,23 @@ class MultiScene:
             raise RtError(f"rt_multi_render: {multi_lib().rt_multi_last_error().decode()}")
         return img, st, ms.value
 
+    def render_frames(self, params, d_outs, stripe_height=16, stats=False):
+        """Renders len(d_outs) frames into device buffers on devices[0] (int pointers) with
+        rt_multi_render_frames (batched launches, two batches in flight); params: one
+        RenderParams or one per frame.  Returns (Stats or None, wall ms)."""
+        n = len(d_outs)
+        plist = params if isinstance(params, (list, tuple)) else [params] * n
+        if len(plist) != n:
+            raise ValueError("one params per output buffer")
+        parr = (abi.RenderParams * n)(*plist)
+        oarr = (C.c_void_p * n)(*[C.c_void_p(d) for d in d_outs])
+        st, ms = (abi.Stats() if stats else None), C.c_double()
+        rc = multi_lib().rt_multi_render_frames(self._h, parr, n, stripe_height, oarr,
+                                                C.byref(st) if st is not None else None, C.byref(ms))
+        if rc != RT_OK:
+            raise RtError(f"rt_multi_render_frames: {multi_lib().rt_multi_last_error().decode()}")
+        return st, ms.value
+
     def close(self):
         if self._h:
             multi_lib().rt_multi_free(self._h)
@@ -454,6 +499,20 @@ class MultiScene:
             self.close()
         except Exception:
             pass
+
+
+def multi_interleave_frames_host(gathered, height, stripe_height, n):
+    """Host restatement of rt_multi's batched assembly: gathered [n, frames, max_rows, W, C] ->
+    [frames, H, W, C]."""
+    g = np.ascontiguousarray(gathered)
+    nf = g.shape[1]
+    out = np.empty((nf, height) + g.shape[3:], dtype=g.dtype)
+    ptrs = (C.c_void_p * nf)(*[C.c_void_p(out[f].ctypes.data) for f in range(nf)])
+    rc = multi_lib().rt_multi_interleave_frames_host(g.ctypes.data_as(C.c_void_p), ptrs, nf, height, g.shape[3],
+                                                     g.shape[4], g.itemsize, stripe_height, n)
+    if rc != RT_OK:
+        raise RtError(f"rt_multi_interleave_frames_host: {multi_lib().rt_multi_last_error().decode()}")
+    return out
 
 
 def multi_interleave_host(gathered, height, stripe_height, n):

@@ -134,14 +134,21 @@ class GenParams(C.Structure):
 
 
 class UploadOptions(C.Structure):
-    _fields_ = [("device_tree", C.c_int), ("reserved_", C.c_int * 7)]
+    """rt_upload_options (include/rt_hip.h); make one with upload_options(**fields)."""
+    _fields_ = [("device_tree", C.c_int), ("build_threads", C.c_int), ("stack_ring", C.c_int),
+                ("lds_treelet", C.c_int), ("collapse", C.c_int), ("sbvh_leaf_max", C.c_int),
+                ("sbvh_bins", C.c_int), ("blocks_per_cu", C.c_int), ("grid_spare", C.c_int),
+                ("verbose", C.c_int), ("sbvh_alpha", C.c_double), ("sbvh_budget", C.c_double),
+                ("sbvh_c_trav", C.c_double), ("collapse_c_tri", C.c_double), ("reserved_", C.c_int * 8)]
 
 
 RT_TREE_SAH, RT_TREE_REFERENCE, RT_TREE_SBVH = 0, 1, 2
+RT_COLLAPSE_GREEDY, RT_COLLAPSE_SAH = 0, 1
 
 # Symbols each library must export (declared in include/*.h).
 HIP_SYMBOLS = {
     "rt_scene_upload": (C.c_int, [C.POINTER(SceneSoA), C.POINTER(BvhSoA), C.c_int, C.POINTER(C.c_void_p)]),
+    "rt_upload_options_init": (None, [C.POINTER(UploadOptions)]),
     "rt_scene_upload_ex": (C.c_int, [C.POINTER(SceneSoA), C.POINTER(BvhSoA), C.c_int, C.POINTER(UploadOptions),
                                      C.POINTER(C.c_void_p)]),
     "rt_scene_upload_multi": (C.c_int, [C.POINTER(SceneSoA), C.POINTER(BvhSoA), C.POINTER(C.c_int), C.c_int,
@@ -197,11 +204,15 @@ MULTI_SYMBOLS = {
     "rt_multi_device_count": (C.c_int, [C.c_void_p]),
     "rt_multi_render": (C.c_int, [C.c_void_p, C.POINTER(RenderParams), C.c_int, C.c_void_p, C.POINTER(Stats),
                                   C.POINTER(C.c_double)]),
+    "rt_multi_render_frames": (C.c_int, [C.c_void_p, C.POINTER(RenderParams), C.c_int, C.c_int,
+                                         C.POINTER(C.c_void_p), C.POINTER(Stats), C.POINTER(C.c_double)]),
     "rt_multi_render_to_host": (C.c_int, [C.c_void_p, C.POINTER(RenderParams), C.c_int, C.c_void_p,
                                           C.POINTER(Stats), C.POINTER(C.c_double)]),
     "rt_multi_max_rows": (C.c_int, [C.c_int, C.c_int, C.c_int]),
     "rt_multi_interleave_host": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                            C.c_int]),
+    "rt_multi_interleave_frames_host": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.c_int, C.c_int, C.c_int,
+                                                  C.c_int, C.c_int, C.c_int, C.c_int]),
     "rt_multi_free": (None, [C.c_void_p]),
     "rt_multi_last_error": (C.c_char_p, []),
 }

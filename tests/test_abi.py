@@ -51,13 +51,16 @@ def test_struct_layouts_match_c(tmp_path):
                "rt_sphere": abi.Sphere, "rt_plane": abi.Plane, "rt_light": abi.Light,
                "rt_camera_def": abi.CameraDef, "rt_camera": abi.Camera, "rt_raw_scene": abi.RawScene,
                "rt_scene_soa": abi.SceneSoA, "rt_bvh_soa": abi.BvhSoA, "rt_render_params": abi.RenderParams,
-               "rt_stats": abi.Stats, "rt_gen_params": abi.GenParams}
-    src = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{ROOT}/include/rt_host.h"', "int main(void){"]
+               "rt_stats": abi.Stats, "rt_gen_params": abi.GenParams, "rt_upload_options": abi.UploadOptions}
+    src = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{ROOT}/include/rt_host.h"',
+           f'#include "{ROOT}/include/rt_hip.h"', "int main(void){"]
     for name in structs:
         src.append(f'printf("{name} %zu\\n", sizeof({name}));')
     src.append('printf("params.out_format %zu\\n", offsetof(rt_render_params, out_format));')
     src.append('printf("soa.mat_shadowable %zu\\n", offsetof(rt_scene_soa, mat_shadowable));')
     src.append('printf("params.lights_ext %zu\\n", offsetof(rt_render_params, lights_ext));')
+    src.append('printf("opt.sbvh_alpha %zu\\n", offsetof(rt_upload_options, sbvh_alpha));')
+    src.append('printf("opt.collapse_c_tri %zu\\n", offsetof(rt_upload_options, collapse_c_tri));')
     src.append("return 0;}")
     (tmp_path / "sizes.c").write_text("\n".join(src))
     subprocess.run(["gcc", "-o", str(tmp_path / "sizes"), str(tmp_path / "sizes.c")], check=True)
@@ -68,6 +71,28 @@ def test_struct_layouts_match_c(tmp_path):
     assert int(got["params.out_format"]) == abi.RenderParams.out_format.offset
     assert int(got["soa.mat_shadowable"]) == abi.SceneSoA.mat_shadowable.offset
     assert int(got["params.lights_ext"]) == abi.RenderParams.lights_ext.offset
+    assert int(got["opt.sbvh_alpha"]) == abi.UploadOptions.sbvh_alpha.offset
+    assert int(got["opt.collapse_c_tri"]) == abi.UploadOptions.collapse_c_tri.offset
+
+
+def test_upload_options_defaults_and_validation():
+    # The library reads no environment: every build / layout choice is an rt_upload_options field.
+    o = abi.UploadOptions()
+    rtamd.hip_lib().rt_upload_options_init(C.byref(o))
+    assert (o.device_tree, o.stack_ring, o.lds_treelet, o.collapse) == (abi.RT_TREE_SBVH, 0, -1, abi.RT_COLLAPSE_GREEDY)
+    assert (o.sbvh_leaf_max, o.sbvh_bins, o.blocks_per_cu, o.grid_spare, o.verbose) == (2, 32, 0, 0, 0)
+    assert (o.sbvh_alpha, o.sbvh_budget, o.sbvh_c_trav, o.collapse_c_tri) == (1e-5, 0.75, 1.0, 1.0)
+    hs = rtamd.HostScene.generate("cornell")
+    hs.prepare()
+    lib = rtamd.hip_lib()
+    for field, bad in (("stack_ring", 12), ("blocks_per_cu", -1), ("sbvh_bins", 1), ("sbvh_leaf_max", 9),
+                       ("device_tree", 7), ("collapse", 3), ("sbvh_alpha", float("nan"))):
+        q = rtamd.upload_options(**{field: bad})
+        rc = lib.rt_scene_upload_ex(hs.soa, hs.bvh, 0, C.byref(q), C.byref(C.c_void_p()))
+        assert rc == abi.RT_ERR_INVALID, (field, rc)
+        assert lib.rt_last_error(), field
+    with pytest.raises(ValueError):
+        rtamd.upload_options(no_such_field=1)
 
 
 def test_hip_entry_points_reject_bad_arguments():

@@ -146,6 +146,7 @@ def test_row_range():
     part, st = dev.render(p)
     assert np.array_equal(part, full[37:90])
     assert st.primary_rays == 53 * 160
+    assert st.pixels == 53 * 160   # rt_stats.pixels: pixels written
 
 
 @pytest.mark.parametrize("w,h", [(1, 1), (13, 7), (8, 8), (9, 1), (1, 17)])
@@ -241,27 +242,33 @@ def test_full_size_office_1080p_parity():
     assert counts(st) == [cnt.primary_rays, cnt.shadow_rays, cnt.reflection_rays]
 
 
-def test_full_size_4k_16spp_every_8th_row():
-    # BASELINE config 3 (3840x2160, 4x4 stratified): every 8th row (1.04 M pixels, 16.6 M
-    # samples) against the oracle, with the exact ray counts of those rows (rendered again as
-    # the 1-row stripe shard 3 of 8), and the exact primary count of the whole frame.
+def test_full_size_4k_16spp_band_and_every_4th_row():
+    # BASELINE config 3 (3840x2160, 4x4 stratified): a contiguous 64-row band through the
+    # middle of the frame plus every 4th row elsewhere (604 rows, 2.3 M pixels, 37 M samples)
+    # against the oracle, the exact ray counts of the every-4th-row set (rendered again as the
+    # 1-row stripe shard 1 of 4: the same rows through the stripe path), and the exact primary
+    # count of the whole frame.
     hs, dev, orc = Case.get("office")
     p = hs.render_params(3840, 2160, 4)
     p.out_format = rtamd.RT_OUT_RGB_F64
     img, st = dev.render(p)
     assert st.primary_rays == 3840 * 2160 * 16
-    ys = np.arange(3, 2160, 8)
+    band = np.arange(1048, 1112)
+    ys = np.union1d(np.arange(1, 2160, 4), band)
     xy = np.stack(np.meshgrid(np.arange(3840), ys), -1).reshape(-1, 2).astype(np.int32)
-    ref, cnt = orc.render_pixels(p, xy, pyoracle.MODE_ORDERED, threads=0)
+    ref, _ = orc.render_pixels(p, xy, pyoracle.MODE_ORDERED, threads=0)
     assert np.abs(img[ys].reshape(-1, 3) - ref).max() <= TOL64
     rng = np.random.default_rng(7)   # and reference-semantics traversal on 3000 random pixels
     xr = np.stack([rng.integers(0, 3840, 3000), rng.integers(0, 2160, 3000)], 1).astype(np.int32)
     ref2, _ = orc.render_pixels(p, xr, pyoracle.MODE_REFERENCE, threads=0)
     assert np.abs(img[xr[:, 1], xr[:, 0]] - ref2).max() <= TOL64
-    p.stripe_height, p.stripe_count, p.stripe_index = 1, 8, 3
-    img8, st8 = dev.render(p)
-    assert np.array_equal(img8, img[ys])
-    assert counts(st8) == [cnt.primary_rays, cnt.shadow_rays, cnt.reflection_rays]
+    y4 = np.arange(1, 2160, 4)
+    xy4 = np.stack(np.meshgrid(np.arange(3840), y4), -1).reshape(-1, 2).astype(np.int32)
+    _, cnt = orc.render_pixels(p, xy4, pyoracle.MODE_ORDERED, threads=0)
+    p.stripe_height, p.stripe_count, p.stripe_index = 1, 4, 1
+    img4, st4 = dev.render(p)
+    assert np.array_equal(img4, img[y4])
+    assert counts(st4) == [cnt.primary_rays, cnt.shadow_rays, cnt.reflection_rays]
 
 
 def test_config4_10m_random_triangles_full_frame():
@@ -296,27 +303,41 @@ def test_config4_10m_random_triangles_full_frame():
     assert dev.debug_counters()["stack_spills"] > 0
 
 
-def test_config5_8k_64spp_one_of_8_shards_every_12th_row():
-    # BASELINE config 5 (7680x4320, 8x8 stratified, rows sharded over 8 GPUs): the shard of
-    # rank 3 renders on this GPU; every 12th of its rows (45 rows, 22 M samples) against the
-    # oracle at their global rows, plus 150 random pixels of the shard.
+def test_config5_8k_64spp_all_8_shards():
+    # BASELINE config 5 (7680x4320, 8x8 stratified, 16-row stripes over 8 GPUs).  Every one of the
+    # 8 shards renders on this GPU as its rank would; the shards are assembled by the library's
+    # restatement of the multi-GPU assembly (rt_multi_interleave_host, the re-interleave kernel's
+    # index map) and must equal the whole frame rendered in one launch bit for bit, with ray counts
+    # adding up.  Against the oracle: in EVERY shard its first, a middle and its last row at full
+    # width (24 rows, 11.8 M samples) and 100 random pixels (reference-semantics traversal).
     hs, dev, orc = Case.get("office")
-    p = hs.render_params(7680, 4320, 8)
-    p.stripe_height, p.stripe_count, p.stripe_index = 16, 8, 3
+    W, H, n, sh = 7680, 4320, 8, 16
+    p = hs.render_params(W, H, 8)
     p.out_format = rtamd.RT_OUT_RGB_F64
-    img, st = dev.render(p)
-    rows = rtamd.shard_rows(4320, 16, 8, 3)
-    assert img.shape == (len(rows), 7680, 3) and st.primary_rays == len(rows) * 7680 * 64
-    q = hs.render_params(7680, 4320, 8)
-    li = np.arange(5, len(rows), 12)
-    xy = np.stack(np.meshgrid(np.arange(7680), rows[li]), -1).reshape(-1, 2).astype(np.int32)
-    ref, _ = orc.render_pixels(q, xy, pyoracle.MODE_ORDERED, threads=0)
-    assert np.abs(img[li].reshape(-1, 3) - ref).max() <= TOL64
+    full, st_full = dev.render(p)
+    assert st_full.primary_rays == W * H * 64
+    mr = rtamd.multi_lib().rt_multi_max_rows(H, sh, n)
+    gathered = np.full((n, mr, W, 3), np.nan)
+    tot = np.zeros(3, np.int64)
+    q = hs.render_params(W, H, 8)
     rng = np.random.default_rng(11)
-    li = rng.integers(0, len(rows), 150)
-    xs = rng.integers(0, 7680, 150)
-    ref, _ = orc.render_pixels(q, np.stack([xs, rows[li]], 1).astype(np.int32), pyoracle.MODE_REFERENCE)
-    assert np.abs(img[li, xs] - ref).max() <= TOL64
+    for g in range(n):
+        p.stripe_height, p.stripe_count, p.stripe_index = sh, n, g
+        img, st = dev.render(p)
+        rows = rtamd.shard_rows(H, sh, n, g)
+        assert img.shape == (len(rows), W, 3) and st.primary_rays == len(rows) * W * 64
+        gathered[g, :len(rows)] = img
+        tot += counts(st)
+        li = np.array([0, len(rows) // 2 + 3, len(rows) - 1])
+        xy = np.stack(np.meshgrid(np.arange(W), rows[li]), -1).reshape(-1, 2).astype(np.int32)
+        ref, _ = orc.render_pixels(q, xy, pyoracle.MODE_ORDERED, threads=0)
+        assert np.abs(img[li].reshape(-1, 3) - ref).max() <= TOL64, g
+        lr, xs = rng.integers(0, len(rows), 100), rng.integers(0, W, 100)
+        ref, _ = orc.render_pixels(q, np.stack([xs, rows[lr]], 1).astype(np.int32), pyoracle.MODE_REFERENCE)
+        assert np.abs(img[lr, xs] - ref).max() <= TOL64, g
+    assert list(tot) == counts(st_full)
+    assembled = rtamd.multi_interleave_host(gathered, H, sh, n)
+    assert np.array_equal(assembled, full)
 
 
 def test_bad_params_fail_loudly():
@@ -369,6 +390,7 @@ def test_adaptive_pass_matches_oracle(kind, kw, w, h):
                           device="cuda")
         st, nsel = dev.launch_adaptive(p, d_prim.data_ptr(), out.data_ptr(), 4, 0.02, stats=True)
         assert nsel == int(sel.sum())
+        assert st.pixels == nsel   # the adaptive pass re-writes the selected pixels
         assert np.abs(out.cpu().numpy().astype(np.float64) - ref).max() <= tol
         assert counts(st) == [cnt.primary_rays, cnt.shadow_rays, cnt.reflection_rays]
 
@@ -630,15 +652,14 @@ def test_device_tree_changes_no_pixel(kind, kw, w, h, spp):
 
 
 @pytest.mark.parametrize("tree", ["sah", "sbvh"])
-def test_tree_independent_of_build_threads(monkeypatch, tree):
+def test_tree_independent_of_build_threads(tree):
     hs = rtamd.HostScene.generate("random_tris", n_triangles=300000, seed=5)
     hs.prepare()
     p = hs.render_params(192, 108, 1)
     p.flags = rtamd.RT_FLAG_WIDE_STATS
     out = []
-    for t in ("1", "7"):
-        monkeypatch.setenv("RT_BUILD_THREADS", t)
-        dev = rtamd.DeviceScene(hs, 0, tree=tree)
+    for t in (1, 7):
+        dev = rtamd.DeviceScene(hs, 0, tree=tree, build_threads=t)
         img, st = dev.render(p)
         out.append((img, st.node_visits, st.tri_tests, dev.device_bytes))
         dev.close()
@@ -647,17 +668,16 @@ def test_tree_independent_of_build_threads(monkeypatch, tree):
 
 @pytest.mark.parametrize("kind,kw,w,h,spp", [("office", {}, 320, 180, 1), ("cornell", {"detail": 3}, 97, 61, 2),
                                              ("random_tris", {"n_triangles": 200000}, 160, 90, 1)])
-def test_stack_ring_depth_changes_no_pixel(monkeypatch, kind, kw, w, h, spp):
+def test_stack_ring_depth_changes_no_pixel(kind, kw, w, h, spp):
     # Scenes of >= 2^18 device triangle records launch the 16-entry LDS stack ring (fewer global spills on deep
-    # trees, a smaller LDS treelet); RT_RING forces either ring on any scene.  Same bits, same
+    # trees, a smaller LDS treelet); the stack_ring upload option forces either ring on any scene.  Same bits, same
     # ray counts, and the deep ring still matches the oracle.
     hs, _, orc = Case.get(kind, **kw)
     p = hs.render_params(w, h, spp)
     p.out_format = rtamd.RT_OUT_RGB_F64
     out = []
-    for ring in ("8", "16"):
-        monkeypatch.setenv("RT_RING", ring)
-        dev = rtamd.DeviceScene(hs, 0)
+    for ring in (8, 16):
+        dev = rtamd.DeviceScene(hs, 0, stack_ring=ring)
         out.append(dev.render(p))
         dev.close()
     (a, sa), (b, sb) = out
@@ -768,20 +788,17 @@ def _split_stress_scene(tmp_path):
     return path
 
 
-def test_spatial_splits_stress_scene_bit_identical(tmp_path, monkeypatch):
+def test_spatial_splits_stress_scene_bit_identical(tmp_path):
     hs = rtamd.HostScene.load(_split_stress_scene(tmp_path))
     hs.prepare()
     p = hs.render_params(96, 72, 2)
     p.out_format = rtamd.RT_OUT_RGB_F64
     out = {}
     for tree in ("sbvh", "sbvh1", "sah", "reference"):
-        # sbvh1: spatial splits with single-reference leaves (RT_SBVH_LEAF=1), so the triangle
+        # sbvh1: spatial splits with single-reference leaves (sbvh_leaf_max=1), so the triangle
         # test count isolates the effect of the splits from SAH leaf termination
-        if tree == "sbvh1":
-            monkeypatch.setenv("RT_SBVH_LEAF", "1")
-        else:
-            monkeypatch.delenv("RT_SBVH_LEAF", raising=False)
-        dev = rtamd.DeviceScene(hs, 0, tree="sbvh" if tree == "sbvh1" else tree)
+        extra = {"sbvh_leaf_max": 1} if tree == "sbvh1" else {}
+        dev = rtamd.DeviceScene(hs, 0, tree="sbvh" if tree == "sbvh1" else tree, **extra)
         img, st = dev.render(p)
         q = rtamd.abi.RenderParams.from_buffer_copy(p)
         q.flags = rtamd.RT_FLAG_WIDE_STATS

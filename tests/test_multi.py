@@ -52,6 +52,28 @@ def test_stripes_gathered_and_interleaved_equal_full_frame(office, w, h, sh, n):
     assert rays == cnt.primary_rays + cnt.shadow_rays + cnt.reflection_rays
 
 
+@pytest.mark.parametrize("w,h,sh,n,nf", [(40, 23, 4, 3, 3), (32, 18, 16, 8, 2), (24, 14, 2, 2, 4)])
+def test_batched_stripes_gathered_and_interleaved_equal_frames(office, w, h, sh, n, nf):
+    # rt_multi_render_frames: GPU g renders its stripes of every frame of a batch (distinct
+    # cameras: an orbit) into one [frames][max_rows] block, one gather stacks the n blocks, and the
+    # batch's assembly kernel (host restatement: same index map) must give every frame exactly.
+    hs, orc = office
+    base = hs.render_params(w, h, 1)
+    cams = [rtamd.camera_orbit(base, 0.1 * f) for f in range(nf)]
+    mr = rtamd.multi_lib().rt_multi_max_rows(h, sh, n)
+    gathered = np.full((n, nf, mr, w, 3), np.nan)   # padding rows must never reach a frame
+    for g in range(n):
+        for f, cam in enumerate(cams):
+            p = rtamd.abi.RenderParams.from_buffer_copy(cam)
+            p.stripe_height, p.stripe_count, p.stripe_index = sh, n, g
+            shard, _ = orc.render(p, pyoracle.MODE_REFERENCE)
+            gathered[g, f, :shard.shape[0]] = shard
+    frames = rtamd.multi_interleave_frames_host(gathered, h, sh, n)
+    for f, cam in enumerate(cams):
+        full, _ = orc.render(cam, pyoracle.MODE_REFERENCE)
+        assert np.array_equal(frames[f], full), f
+
+
 def test_interleave_rejects_bad_arguments():
     g = np.zeros((2, 3, 4, 3), np.float32)
     with pytest.raises(rtamd.RtError):
@@ -73,6 +95,30 @@ def test_multi_driver_one_gpu_equals_single_launch(gpu_available, office, fmt):
         assert [st.primary_rays, st.shadow_rays, st.reflection_rays] == \
             [rst.primary_rays, rst.shadow_rays, rst.reflection_rays]
         assert ms > 0
+    m.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nf,w,h,sh", [(5, 320, 180, 16), (2, 97, 61, 4), (1, 64, 48, 8)])
+def test_multi_driver_frames_equal_single_launches(gpu_available, office, nf, w, h, sh):
+    # Batched multi-GPU entry on the box's one GPU (one RCCL rank): batches of frames, two in
+    # flight on separate streams / communicators, every frame equal to its own single launch.
+    import torch
+    hs, _ = office
+    m = rtamd.MultiScene(hs, devices=(0,))
+    dev = rtamd.DeviceScene(hs, 0)
+    base = hs.render_params(w, h, 1)
+    base.out_format = rtamd.RT_OUT_RGB_F64
+    cams = [rtamd.camera_orbit(base, 0.05 * f) for f in range(nf)]
+    outs = [torch.full((h, w, 3), float("nan"), dtype=torch.float64, device="cuda") for _ in range(nf)]
+    st, ms = m.render_frames(cams, [o.data_ptr() for o in outs], stripe_height=sh, stats=True)
+    rays = 0
+    for f, cam in enumerate(cams):
+        ref, rst = dev.render(cam)
+        assert np.array_equal(outs[f].cpu().numpy(), ref), f
+        rays += rst.primary_rays + rst.shadow_rays + rst.reflection_rays
+    assert st.primary_rays + st.shadow_rays + st.reflection_rays == rays
+    assert st.pixels == nf * w * h and ms > 0
     m.close()
 
 

@@ -7,5 +7,4 @@ O=gpurun_out/configs_probe.txt
 timeout -k 10 300 python tools/shard_probe.py | tee -a $O
 timeout -k 10 300 python tools/perf_probe.py office:3840x2160:4 random_tris:1920x1080:1:10000000 | tee -a $O
 timeout -k 10 300 python tools/perf_probe.py random_tris:1920x1080:1:1000000 | tee -a $O
-RT_DEVICE_TREE=sah timeout -k 10 300 python tools/perf_probe.py random_tris:1920x1080:1:1000000 | sed 's/^/[sah] /' | tee -a $O
 timeout -k 10 300 python tools/config5_probe.py | tee -a $O

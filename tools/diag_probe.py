@@ -6,7 +6,7 @@ import rtamd  # noqa: E402
 
 kind = sys.argv[1] if len(sys.argv) > 1 else "office"
 w, h, spp = (int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])) if len(sys.argv) > 4 else (1920, 1080, 1)
-kw = {"n_triangles": 1000000} if kind == "random_tris" else {}
+kw = {"n_triangles": int(sys.argv[5]) if len(sys.argv) > 5 else 1000000} if kind == "random_tris" else {}
 host = rtamd.HostScene.generate(kind, **kw)
 host.prepare()
 gpu = rtamd.DeviceScene(host, 0)
@@ -26,6 +26,7 @@ for flags, name in [(rtamd.RT_FLAG_WIDE_STATS, "4-wide"), (rtamd.RT_FLAG_TRAVERS
     print(f"  leaf loop: {d['leaf_iters']} wave-iters, SIMD eff {d['leaf_lanes']/(64*max(1,d['leaf_iters'])):.3f}")
     print(f"  trav rounds: {d['trav_rounds']}, lanes active {d['trav_round_lanes']/(64*max(1,d['trav_rounds'])):.3f}; outer iters {d['outer_iters']}")
     print(f"  cycles: trav {d['trav_cycles']/tot:.3f} shade {d['shade_cycles']/tot:.3f} fetch {d['fetch_cycles']/tot:.3f} (total wave-cycles {tot:.3e})")
+    print(f"  stack spills {d['stack_spills']} ({d['stack_spills']/rays:.3f} per ray)")
     print(f"  per ray: node wave-iters {d['node_iters']*64/rays:.1f}  leaf wave-iters {d['leaf_iters']*64/rays:.1f}")
     it = d['node_iters'] + d['leaf_iters']
     print(f"  trav cycles per wave-iteration {d['trav_cycles']/max(1,it):.0f}; trav rounds {d['trav_rounds']}, "

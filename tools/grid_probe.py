@@ -1,6 +1,6 @@
 """Frame time vs persistent-grid size (dev tool): one frame per launch and 32 frames per
-launch, office 1080p, for RT_BLOCKS_PER_CU = 1..4 (set per process: run once per value).
-usage: RT_BLOCKS_PER_CU=k python tools/grid_probe.py"""
+launch, office 1080p, with at most k persistent blocks per CU (blocks_per_cu upload option).
+usage: python tools/grid_probe.py k"""
 import os
 import sys
 
@@ -12,7 +12,8 @@ import rtamd  # noqa: E402
 
 host = rtamd.HostScene.generate("office")
 host.prepare()
-gpu = rtamd.DeviceScene(host, 0)
+K = int(sys.argv[1]) if len(sys.argv) > 1 else 0
+gpu = rtamd.DeviceScene(host, 0, blocks_per_cu=K)
 p = host.render_params(1920, 1080, 1)
 for F in (1, 32):
     outs = [torch.zeros((1080, 1920, 3), device="cuda") for _ in range(F)]
@@ -26,4 +27,4 @@ for F in (1, 32):
         torch.cuda.synchronize()
         ms.append(e0.elapsed_time(e1))
     m = float(np.median(ms))
-    print(f"blocks/CU {os.environ.get('RT_BLOCKS_PER_CU', 'max')} F={F}: {m:.3f} ms, {m / F:.4f} ms/frame", flush=True)
+    print(f"blocks/CU {K or 'max'} F={F}: {m:.3f} ms, {m / F:.4f} ms/frame", flush=True)

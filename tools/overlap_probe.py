@@ -1,6 +1,6 @@
 """Can another kernel run beside the persistent render kernel? (dev tool, under gpurun)  Stream A
 renders a 32-frame launch; stream B, enqueued right after, copies 1 GB device to device (a
-stand-in for the RCCL gather of the previous launch).  Prints, per RT_GRID_SPARE setting, when B
+stand-in for the RCCL gather of the previous launch).  Prints, per grid_spare upload option, when B
 ends relative to A's start and end (ms)."""
 import json
 import os
@@ -23,7 +23,7 @@ y = torch.empty_like(x)
 sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
 res = {}
 for spare in [0, 4, 16, 64, 0, 4, 16, 64]:
-    os.environ["RT_GRID_SPARE"] = str(spare)
+    gpu = rtamd.DeviceScene(host, 0, grid_spare=spare)
     torch.cuda.synchronize()
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
     with torch.cuda.stream(sa):
