@@ -72,7 +72,10 @@ def parse():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=1, help="n: n*n stratified samples per pixel")
     ap.add_argument("--tris", type=int, default=0, help="random_tris triangle count")
-    ap.add_argument("--cpu-row-stride", type=int, default=1, help="cpu_baseline renders every k-th row")
+    ap.add_argument("--cpu-row-stride", type=int, default=0,
+                    help="cpu_baseline renders every k-th row (default: 1, or 16 when one whole frame would take "
+                         "longer than --cpu-seconds on this host, e.g. BASELINE configs 3-5; the frame time is then "
+                         "extrapolated from the sample)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="cpu_baseline: minimum timed CPU work")
     ap.add_argument("--cpu-threads", type=int, default=0,
@@ -362,6 +365,8 @@ def main():
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(ms_per_step, 4),
+            # the render kernel's own time per frame (HIP events around each launch / its frames)
+            "kernel_ms_per_frame": round(kernel_ms_avg / frames_per_launch, 4),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -416,51 +421,65 @@ def default_frames(a):
     return int(min(128, max(1, 2 ** round(math.log2(max(1.0, 2.6e8 / samples))))))
 
 
-def pmc_per_frame(key, frames_per_launch=None):
-    """HBM bytes per frame of this workload from the newest committed rocprofv3 --pmc summary
-    (profiles/r*/pmc_*.json, tools/pmc_summary.py: production-kernel FETCH_SIZE / WRITE_SIZE summed
-    over the profiled run's dispatches, divided by the frames they rendered, with the access-width
-    corrections of profiles/r*/hbm_calib.json), preferring one profiled at the same frames per
-    launch (fewer frames per launch read more per frame: the L2 starts cold each launch); None when
-    this workload was not profiled."""
-    best, best_same = None, None
-    for path in sorted(ROOT.glob("profiles/r*/pmc_*.json")):
+def _profile_tag(path):
+    """Profiling round of a committed summary, from its name (pmc_office1080_r02u_f20.json -> "r02u",
+    pmc_rt10m_r03c.json -> "r03c"): later rounds and later letters sort higher."""
+    import re
+    m = re.search(r"_(r\d\d[a-z]*)(?:_|\.json$)", path.name)
+    return m.group(1) if m else ""
+
+
+def _newest_first(key):
+    """Committed PMC summaries of this workload, newest profiling round first."""
+    found = []
+    for path in ROOT.glob("profiles/r*/pmc_*.json"):
         try:
             d = json.loads(path.read_text())
         except (OSError, ValueError):
             continue
-        if d.get("_workload") != key:
-            continue
+        if d.get("_workload") == key:
+            found.append((_profile_tag(path), str(path), d))
+    found.sort(reverse=True)
+    return [(Path(p), d) for _, p, d in found]
+
+
+def pmc_per_frame(key, frames_per_launch=None):
+    """HBM bytes per frame of this workload from the newest committed rocprofv3 --pmc summary
+    (profiles/r*/pmc_*.json, tools/pmc_summary.py: production-kernel FETCH_SIZE / WRITE_SIZE summed
+    over the profiled run's dispatches, divided by the frames they rendered, with the access-width
+    corrections of profiles/r*/hbm_calib.json).  Among the summaries of the newest profiling round
+    that has one, a summary profiled at the same frames per launch wins (fewer frames per launch
+    read more per frame: the L2 starts cold each launch); None when this workload was not
+    profiled."""
+    cands = []
+    for path, d in _newest_first(key):
         pf = d.get("_per_frame", {})
         if "hbm_read_bytes" in pf and "hbm_write_bytes" in pf:
-            best = {"read": pf["hbm_read_bytes"], "write": pf["hbm_write_bytes"],
-                    "td_busy_frac": d.get("_derived", {}).get("td_busy_frac"),
-                    "source": str(path.relative_to(ROOT))}
-            if frames_per_launch is not None and d.get("_bench", {}).get("frames_per_launch") == frames_per_launch:
-                best_same = best
-    return best_same or best
+            cands.append((_profile_tag(path), path, d, pf))
+    if not cands:
+        return None
+    newest = cands[0][0]
+    same_round = [c for c in cands if c[0] == newest]
+    pick = next((c for c in same_round if frames_per_launch is not None
+                 and c[2].get("_bench", {}).get("frames_per_launch") == frames_per_launch), same_round[0])
+    _, path, d, pf = pick
+    return {"read": pf["hbm_read_bytes"], "write": pf["hbm_write_bytes"],
+            "td_busy_frac": d.get("_derived", {}).get("td_busy_frac"), "source": str(path.relative_to(ROOT))}
 
 
 def pmc_wave_mix(key):
     """Where a wave's cycles go (rocprofv3 SQ counters of this workload, newest committed summary):
     issuing an instruction, waiting on a memory counter, the rest (ready behind the SIMD's other
     waves); None when no such pass was committed."""
-    best = None
-    for path in sorted(ROOT.glob("profiles/r*/pmc_*.json")):
-        try:
-            d = json.loads(path.read_text())
-        except (OSError, ValueError):
-            continue
-        if d.get("_workload") != key:
-            continue
+    for path, d in _newest_first(key):
         try:
             wc = d["SQ_WAVE_CYCLES"]["sum"]
             issue, wait = d["SQ_ACTIVE_INST_ANY"]["sum"] / wc, d["SQ_WAIT_ANY"]["sum"] / wc
         except (KeyError, TypeError, ZeroDivisionError):
             continue
-        best = {"issue_frac": round(issue, 3), "mem_wait_frac": round(wait, 3),
+        return {"issue_frac": round(issue, 3), "mem_wait_frac": round(wait, 3),
                 "other_frac": round(1.0 - issue - wait, 3), "source": str(path.relative_to(ROOT))}
-    return best
+    return None
 
 
 def usable_cpus():
@@ -485,10 +504,19 @@ def cpu_baseline(host, params, a):
     # README.md:10); on the GPU box that is the job's share of the node, not the node's nproc
     threads = a.cpu_threads or usable_cpus()
     orc = pyoracle.Oracle(host.raw, host)
-    ys = np.arange(0, a.height, a.cpu_row_stride)
+    p = host.render_params(a.width, a.height, a.spp)
+    stride = a.cpu_row_stride
+    if stride <= 0:
+        # probe: one 64th of the rows; a whole frame that would exceed --cpu-seconds is sampled
+        # every 16th row (configs 3-5 on a 1/16-row subsample, frame time extrapolated)
+        ys = np.arange(0, a.height, 64)
+        xy = np.stack(np.meshgrid(np.arange(a.width), ys), -1).reshape(-1, 2)
+        t = time.perf_counter()
+        orc.render_pixels(p, xy, pyoracle.MODE_REFERENCE, threads)
+        stride = 16 if (time.perf_counter() - t) * 64 > a.cpu_seconds else 1
+    ys = np.arange(0, a.height, stride)
     xs = np.arange(a.width)
     xy = np.stack(np.meshgrid(xs, ys), -1).reshape(-1, 2)
-    p = host.render_params(a.width, a.height, a.spp)
     rays, frames = 0, 0
     t0 = time.perf_counter()
     while True:
@@ -511,9 +539,15 @@ def cpu_baseline(host, params, a):
         "unit": "Mrays/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{frames} x (every {a.cpu_row_stride}th row of the frame: {len(xy)} pixels), {rays} rays, "
+        "sample": f"{frames} x (every {stride}th row of the frame: {len(xy)} pixels), {rays} rays, "
                   f"{dt:.2f} s; reference-CPU-semantics oracle (recursive unordered fp64 BVH, "
                   f"closest-hit shadows, OpenMP over pixels)",
+        "workload": f"{a.scene} {a.width}x{a.height} spp={a.spp * a.spp}" + (f" tris={a.tris}" if a.tris else ""),
+        "row_stride": stride,
+        # seconds per whole frame at this rate: measured when the sample is whole frames, else
+        # extrapolated from the 1/stride-row sample (rays per frame ~ stride x sample rays)
+        "frame_s": round(dt / frames * stride, 3),
+        "frame_s_extrapolated": stride > 1,
         "cpu_model": cpu_model,
         "nproc": os.cpu_count(),
         "usable_cpus": usable_cpus(),

@@ -136,6 +136,15 @@ __device__ __forceinline__ double buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t voff
 __device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, double x) {
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, x), r, voff, soff, 0);
 }
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+struct D2 {
+  double a, b;
+};
+__device__ __forceinline__ D2 buf_ld2(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+  return D2{__builtin_bit_cast(double, u32x2_t{v.x, v.y}), __builtin_bit_cast(double, u32x2_t{v.z, v.w})};
+}
+// (no b128 store helper: path-state stores are b64, see ST4 in render_kernel)
 
 
 // Lane of the k-th (0-based) set bit of m (k < popcount(m)).
@@ -199,7 +208,7 @@ struct KParams {
   unsigned long long* ctr;
   unsigned long long* heads;  // work head h at heads[h * kHeadStride]
   unsigned long long* wctr;   // per wave {primary, shadow, reflection, 0} rays (plain stores at exit)
-  double* pstate;       // path state, [nslots / 64][kFields][64] fp64
+  double* pstate;       // path state, [nslots / 64][kRegions][64 lanes][4] fp64
   uint32_t* spill;      // [stack_words][nslots] traversal-stack entries below the LDS ring
   unsigned long long* wavelog;  // STATS: per wave {start, last refill, end, pixels} (s_memrealtime)
   unsigned long long* tl;       // TL: per wave and traversal round {start, end, lanes, iterations}
@@ -352,21 +361,23 @@ __device__ __forceinline__ TriOps load_tri(const GTri* tris, uint32_t i) {
   return T;
 }
 
-// Path state kept in global memory between a lane's rays, wave-interleaved
-// [wave][field][64 lanes] fp64: one field access of a wave is one b64 buffer instruction over
-// 512 contiguous bytes.  Only what cannot be recomputed or kept in the LDS slot is kept (the
-// normal of the bounce being shaded lives in the slot's aux words, below):
-//   the textured diffuse colour (HD; untextured hits re-read the material's kd);
-//   the light sum across shadow batches (LACC; a bounce whose lights fit one batch restarts
-//     from the recomputed ambient term);
-//   the sample's colour and weight across mirror bounces (SCOL, W) and the pixel's sum
-//     across samples (PCOL).
-// The mirror coefficient comes from the material (the lane keeps the mesh id).  (16-B slots
-// with b128 accesses were tried: no faster, and some pixels of mirror chains read stale
-// path state under some code layouts -- DESIGN.md §4.)
-enum : int {
-  F_SCOL = 0, F_W = 3, F_PCOL = 4, F_HD = 7, F_LACC = 10, kFields = 13
-};
+// Path state kept in global memory between a lane's rays: per wave kRegions regions of
+// [64 lanes][4 fp64], so a lane's record of a region is ONE 32-B sector, read with two b128 and
+// written with four b64 buffer accesses at the lane offset (one VGPR) plus the region's offset
+// (an SGPR constant).  A lane's store dirties whole sectors: the L2 writes back 32 B per lane
+// and region instead of four partly written 32-B sectors of four field-major arrays (round 2:
+// 13 field-major fp64 arrays, HBM writes 56.6 MB per office frame against a 24.9 MB image;
+// DESIGN.md §4 "path state").  Only what cannot be recomputed or kept in the LDS slot:
+//   the sample's colour and weight across mirror bounces (R_SCOLW: SCOL xyz, W);
+//   the pixel's sum across samples (R_PCOL, spp > 1);
+//   the textured diffuse colour (R_HD; untextured hits re-read the material's kd);
+//   the light sum across shadow batches of more than 32 lights (R_LACC; a bounce whose lights
+//     fit one batch restarts from the recomputed ambient term).
+// The mirror coefficient comes from the material (the lane keeps the mesh id); the normal of
+// the bounce being shaded lives in the slot's aux words (below).
+enum : int { R_SCOLW = 0, R_PCOL = 1, R_HD = 2, R_LACC = 3, kRegions = 4 };
+constexpr uint32_t kLaneRec = 32;                 // bytes per lane and region
+constexpr uint32_t kRegionBytes = 64 * kLaneRec;  // 2 KB per wave and region
 
 // LDS slots ([field][thread], conflict-free): the ray (the only hand-over between the
 // shading phase, which writes the next ray, and the traversal phase, which reads it) and
@@ -453,24 +464,38 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
 
   const int lane = threadIdx.x & 63;
   const unsigned long long lane_below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  // path state, wave-interleaved [wave][field][64 lanes] (see kFields): buffer ops with the
-  // lane offset in one VGPR and the field offset f*512 as an SGPR constant.
+  // path state, [wave][region][64 lanes][4 fp64] (see kRegions): b128 buffer ops with the lane
+  // offset in one VGPR and the region offset as an SGPR constant.
   const __amdgpu_buffer_rsrc_t prs =
-      __builtin_amdgcn_make_buffer_rsrc(P.pstate, 0, (int)(P.nslots * kFields * sizeof(double)), kBufWord3);
+      __builtin_amdgcn_make_buffer_rsrc(P.pstate, 0, (int)(P.nslots * kRegions * kLaneRec), kBufWord3);
   // (a lane handed over by tail compaction keeps its pixel's path state: pvo travels with it)
-  uint32_t pvo = ((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * (uint32_t)kFields * 64u + (uint32_t)lane) * 8u;
-  auto LDF = [&](int f) { return buf_ld(prs, pvo, (uint32_t)f * 512u); };
-  auto STF = [&](int f, double v) { buf_st(prs, pvo, (uint32_t)f * 512u, v); };
-  auto LDV = [&](int f) { return d3(LDF(f), LDF(f + 1), LDF(f + 2)); };
-  auto STV = [&](int f, D3 v) { STF(f, v.x); STF(f + 1, v.y); STF(f + 2, v.z); };
+  uint32_t pvo = (blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * (uint32_t)kRegions * kRegionBytes +
+                 (uint32_t)lane * kLaneRec;
+  // a region's record: (x, y) at +0, (z, w) at +16 -- one 32-B sector
+  // loads: two b128; stores: four b64.  A buffer store of more than 64 bits reads its data VGPRs
+  // over more than one cycle, and a VALU write of those VGPRs right after it needs one wait state
+  // -- which the compiler does not insert when the store's soffset is an SGPR (as here: the
+  // region offset), so a b128 store lost the high half of z whenever the scheduler put such a
+  // write next to it (round 2's "stale path-state reads"; DESIGN.md §4, tools/isa_audit.py).
+  // 8-byte stores have no such hazard; the four of them fill the record's 32-B sector.
+  auto LD4 = [&](int r, D3& v, double& w) {
+    const D2 a = buf_ld2(prs, pvo, (uint32_t)r * kRegionBytes), b = buf_ld2(prs, pvo, (uint32_t)r * kRegionBytes + 16u);
+    v = d3(a.a, a.b, b.a);
+    w = b.b;
+  };
+  auto ST4 = [&](int r, D3 v, double w) {
+    const uint32_t o = (uint32_t)r * kRegionBytes;
+    buf_st(prs, pvo, o, v.x); buf_st(prs, pvo, o + 8u, v.y); buf_st(prs, pvo, o + 16u, v.z); buf_st(prs, pvo, o + 24u, w);
+  };
+  auto LDV = [&](int r) { D3 v; double w; LD4(r, v, w); return v; };
+  auto STV = [&](int r, D3 v) { ST4(r, v, 0.0); };   // the whole sector (no partial write)
   auto LD_HN = [&]() { return d3(*R.a[0], *R.a[1], *R.a[2]); };
   auto ST_HN = [&](D3 v) { *R.a[0] = v.x; *R.a[1] = v.y; *R.a[2] = v.z; };
   // colour and weight carried across mirror bounces
   auto LD_SCOL_W = [&](D3& scol, double& w) {
-    scol = LDV(F_SCOL);
-    w = LDF(F_W);
+    LD4(R_SCOLW, scol, w);
   };
-  auto ST_SCOL_W = [&](D3 scol, double w) { STV(F_SCOL, scol); STF(F_W, w); };
+  auto ST_SCOL_W = [&](D3 scol, double w) { ST4(R_SCOLW, scol, w); };
 
   // wave-uniform work-head cursor; in list mode the work count comes from the device
   const long long n_list = P.list ? (long long)*P.list_count * P.nsamp : 0;   // work items
@@ -1083,7 +1108,8 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
 
     // ---- tail compaction: donate (sparse wave, queue empty) or adopt pooled lanes ----
     if (heads_left == 0) {
-      const int wib = threadIdx.x >> 6;   // wave in block
+      // wave in block, wave-uniform (an SGPR: derived at the use, not a VGPR held across the loop)
+      const int wib = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
       const bool owner = (state == ST_CLOSEST || state == ST_SHADOW);
       const unsigned long long O = __ballot(owner);
       if (O != 0ull && __popcll(O) <= kDonateMax && *pool_live >= 2u) {
@@ -1223,11 +1249,11 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
         }
         hn = LD_HN();
         const GMat& M = P.mats[mesh];
-        const D3 hdiff = M.tex_w > 0 ? LDV(F_HD) : d3(M.kd[0], M.kd[1], M.kd[2]);
+        const D3 hdiff = M.tex_w > 0 ? LDV(R_HD) : d3(M.kd[0], M.kd[1], M.kd[2]);
         mirror = M.mirror;
         // first batch: the ambient term (mytracer.cpp:574-576) again, else the stored sum
         D3 lacc = light == 0 ? d3(0.0 + P.amb[0] * M.ka[0], 0.0 + P.amb[1] * M.ka[1], 0.0 + P.amb[2] * M.ka[2])
-                             : LDV(F_LACC);
+                             : LDV(R_LACC);
         const uint32_t vw = lvis[threadIdx.x];
         for (int j = light; j < batch_end; ++j) {
           const bool occluded = (j == light) ? shadow_hit : (((vw >> (j - light)) & 1u) != 0u);
@@ -1237,7 +1263,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
         }
         light = batch_end;
         if (light < P.n_lights) {
-          STV(F_LACC, lacc);
+          STV(R_LACC, lacc);
           launch_batch(mirror);
         } else {   // bounce complete (subtrace, mytracer.cpp:546-555)
           D3 s0 = d3(0, 0, 0);
@@ -1338,7 +1364,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
           if (M.shadowable && P.n_lights > 0) {   // shadow rays, mytracer.cpp:589-600
             ST_HN(hn);
             *R.tlim = thit;   // the slot keeps the closest-hit ray and its distance
-            if (M.tex_w > 0) STV(F_HD, hdiff);
+            if (M.tex_w > 0) STV(R_HD, hdiff);
             launch_batch(mirror);
           } else {
             for (int j = 0; j < P.n_lights; ++j) lacc = add(lacc, contrib_of(j, hp, hn, hview, hdiff, M));
@@ -1367,13 +1393,15 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
         so[0] = c.x; so[1] = c.y; so[2] = c.z;
         state = heads_left > 0 ? ST_FETCH : ST_DONE;
       } else if (finish) {
-        const D3 pcol = add(sample == 0 ? d3(0, 0, 0) : LDV(F_PCOL), scol);
+        const D3 pcol = add(sample == 0 ? d3(0, 0, 0) : LDV(R_PCOL), scol);
         sample++;
         if (sample < P.spp_n * P.spp_n) {
-          STV(F_PCOL, pcol);
+          STV(R_PCOL, pcol);
           start_sample();
         } else {   // compute_image: average, clamp, store (mytracer_gpu.cu:155-159, 221-227)
-          const double nn = (double)(P.spp_n * P.spp_n);
+          int n2 = P.spp_n * P.spp_n;
+          asm volatile("" : "+s"(n2));   // converted here, not hoisted into a VGPR live across the loop
+          const double nn = (double)n2;
           const double r = stdmin(pcol.x / nn, 1.0), g = stdmin(pcol.y / nn, 1.0), b = stdmin(pcol.z / nn, 1.0);
           const size_t o = 3 * ((size_t)lrow * P.W + px);
           if (P.out_fmt == RT_OUT_RGB_F64) {
@@ -1696,7 +1724,7 @@ struct LaunchCtx {
   unsigned long long* d_ctr = nullptr;       // [kCtrWords] work heads, stats, diagnostics, then
                                              // FrameDesc[kMaxFrames] (one H2D copy per launch)
   unsigned char* h_ctl = nullptr;            // pinned staging of the same bytes
-  double* d_pstate = nullptr;                // path state, nslots x kFields fp64
+  double* d_pstate = nullptr;                // path state, nslots x kRegions x 32 B
   uint32_t* d_spill = nullptr;               // [stack_words][nslots] (only when stack_words > kShortStack)
   unsigned long long* d_wavelog = nullptr;   // [nslots / 64][4]
   unsigned long long* d_wctr = nullptr;      // [nslots / 64][4] per-wave ray counts
@@ -1864,7 +1892,7 @@ int upload_image(const SceneImage& I, const rt_upload_options& opt, int device, 
   sc->light_cap = RT_MAX_LIGHTS;
   sc->bytes += (long long)(RT_MAX_LIGHTS * 6 * sizeof(double));
   for (LaunchCtx& c : sc->ctx) {
-    const size_t pb = sc->nslots * kFields * sizeof(double);
+    const size_t pb = sc->nslots * kRegions * kLaneRec;
     const size_t wb = sc->nslots / 64 * 4 * sizeof(unsigned long long);
     const size_t sb = sc->stack_words > kShortStack ? sc->nslots * (size_t)sc->stack_words * sizeof(uint32_t) : 0;
     if (hipMalloc(reinterpret_cast<void**>(&c.d_ctr), kCtlBytes) != hipSuccess ||

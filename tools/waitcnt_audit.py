@@ -67,6 +67,13 @@ def audit(body, max_depth=6):
                 continue
             op = l.split()[0]
             operands = l[len(l) - len(l.lstrip()) + len(op):]
+            lm = LOAD.match(l)
+            if lm:   # a later load into the same registers: vector-memory loads return in order, so
+                     # it lands after this one and the earlier value is dead (a legal WAW)
+                ldst = set(range(int(lm.group(3)), int(lm.group(4)) + 1)) if lm.group(3) else {int(lm.group(5))}
+                addr = regs(operands.split(",", 1)[1]) if "," in operands else set()
+                if ldst & dst and not (addr & dst):
+                    return
             if dst & regs(operands) and not op.startswith("s_"):
                 problems.append((i, l.strip(), n_after))
                 return
@@ -97,5 +104,6 @@ if __name__ == "__main__":
     body = kernel_lines(path, sub)
     n, probs = audit(body)
     print(f"{sub}: {len(body)} instructions, {n} vector-memory loads checked, {len(probs)} uses without a covering vmcnt")
+    sys.exit(1 if probs else 0)
     for i, l, k in probs[:20]:
         print(f"  line {i}: {l}   ({k} vmem ops issued after the load)")
