@@ -100,6 +100,8 @@ def parse():
                     help="N > 1: nccl (RCCL over xGMI, the measured path) or gloo (host-staged rehearsal)")
     ap.add_argument("--tree", choices=["sah", "sbvh", "reference"], default=os.environ.get("RT_BENCH_TREE", "sbvh"),
                     help="device traversal hierarchy (pixels identical either way; DESIGN.md §4)")
+    ap.add_argument("--opt", action="append", default=[], metavar="FIELD=VALUE",
+                    help="dev A/B: an rt_upload_options field (e.g. lds_treelet=9); pixels are identical")
     ap.add_argument("--analytic", action="store_true",
                     help="also trace the scene's spheres/planes (always on for --scene spheres)")
     ap.add_argument("--adaptive", action="store_true",
@@ -139,8 +141,9 @@ def main():
     gen = {"n_triangles": a.tris} if a.scene == "random_tris" and a.tris else {}
     host = rtamd.HostScene.generate(a.scene, **gen)
     build_s = host.prepare()
+    upload_opts = {k: (float(v) if "." in v else int(v)) for k, v in (o.split("=", 1) for o in a.opt)}
     gpu = rtamd.DeviceScene(host, device=dev, analytic=a.analytic or a.scene == "spheres",
-                             tree=a.tree)
+                             tree=a.tree, **upload_opts)
     params = host.render_params(a.width, a.height, a.spp)
     params.stripe_height = STRIPE_H
     params.stripe_count = n
@@ -397,6 +400,7 @@ def main():
                 "production_frames_rendered": (F + rem + 1 + a.warmup + a.steps + (a.single_frames if single else 0)
                                                if not a.adaptive else None),
                 "device_scene_MB": round(gpu.device_bytes / 1e6, 1),
+                **({"upload_options": upload_opts} if upload_opts else {}),
             },
             "single_frame": single,
             "roofline": roof,

@@ -123,6 +123,35 @@ def test_multi_driver_frames_equal_single_launches(gpu_available, office, nf, w,
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("nf", [1, 3])
+def test_multi_driver_two_gpus_equal_single_launch(gpu_available, office, nf):
+    # The N > 1 path proper: grouped ncclGather of several GPUs' padded stripe buffers,
+    # per-device streams, re-interleave on devices[0].  Needs a multi-GPU node (the one-GPU
+    # box skips it; INTEGRATION.md "Verification status of the N > 1 path").
+    import torch
+    n = torch.cuda.device_count()
+    if n < 2:
+        pytest.skip("needs >= 2 GPUs")
+    hs, _ = office
+    devs = tuple(range(min(n, 8)))
+    m = rtamd.MultiScene(hs, devices=devs)
+    dev = rtamd.DeviceScene(hs, 0)
+    base = hs.render_params(160, 97, 1)
+    base.out_format = rtamd.RT_OUT_RGB_F64
+    cams = [rtamd.camera_orbit(base, 0.05 * f) for f in range(nf)]
+    outs = [torch.full((97, 160, 3), float("nan"), dtype=torch.float64, device="cuda:0") for _ in range(nf)]
+    st, ms = m.render_frames(cams, [o.data_ptr() for o in outs], stripe_height=4, stats=True)
+    rays = 0
+    for f, cam in enumerate(cams):
+        ref, rst = dev.render(cam)
+        assert np.array_equal(outs[f].cpu().numpy(), ref), f
+        rays += rst.primary_rays + rst.shadow_rays + rst.reflection_rays
+    assert st.primary_rays + st.shadow_rays + st.reflection_rays == rays
+    assert st.pixels == nf * 160 * 97 and ms > 0
+    m.close()
+
+
+@pytest.mark.gpu
 def test_multi_driver_rejects_duplicate_devices(gpu_available, office):
     hs, _ = office
     with pytest.raises(rtamd.RtError, match="distinct"):
