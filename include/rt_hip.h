@@ -99,7 +99,13 @@ enum {
   RT_FLAG_TRAVERSAL_STATS = 1, /* canonical counters: 2-wide traversal (the one the oracle replicates),
                                   counts node visits / triangle tests / closest hits */
   RT_FLAG_WIDE_STATS = 2,      /* same counters on the production 4-wide traversal (diagnostics) */
-  RT_FLAG_TIMELINE = 4         /* production kernel + per-round timeline (diagnostics, rt_debug_timeline) */
+  RT_FLAG_TIMELINE = 4,        /* production kernel + per-round timeline (diagnostics, rt_debug_timeline) */
+  RT_FLAG_TILE_COST = 8,       /* diagnostics: per-tile cost of the launch (rt_debug_tile_cost): bounces */
+  RT_FLAG_TILE_COST_TIME = 16, /* ... the same, as pixel lifetimes (10-ns ticks) */
+  RT_FLAG_COST_ORDER = 32      /* work order: every work head renders the tiles that cost most in the previous
+                                  RT_FLAG_COST_ORDER launch of the same image geometry first (animation: frame
+                                  i's costs order frame i + 1), and this launch's costs are kept for the next;
+                                  shortens the end-of-launch drain; pixels are unchanged */
 };
 
 /* One render call.  Rows are rendered as interleaved stripes:
@@ -330,6 +336,15 @@ int rt_debug_blocks_per_cu(rt_scene* scene, int variant);
  * | the round's setup time << 32.  Unused records are zero.  Synchronises the device; returns
  * words copied. */
 long long rt_debug_timeline(rt_scene* scene, unsigned long long* out, long long n);
+
+/* Diagnostics (tile-order experiments): the per-tile-position cost map of the last launch with
+ * RT_FLAG_TILE_COST / RT_FLAG_TILE_COST_TIME / RT_FLAG_COST_ORDER (index ty * tiles_x + tx over the
+ * shard's 8x8 tiles; per finished sample its bounces + 1, or per pixel its lifetime in 10-ns ticks;
+ * summed over the launch's frames) into out[0..n); returns the number of positions, 0 if none. */
+long long rt_debug_tile_cost(rt_scene* scene, unsigned int* out, long long n);
+/* Diagnostics: launches with exactly n tiles take linear tile order[w / 64] for work item w (a
+ * permutation; pixels do not depend on it); n = 0 clears. */
+int rt_debug_set_tile_order(rt_scene* scene, const unsigned int* order, long long n);
 
 void rt_scene_free(rt_scene* scene);
 

@@ -133,8 +133,23 @@ typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ double buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
   return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
 }
+// measurement-only builds (make variant V=-DRT_DBG_NO_IMAGE_ST / -DRT_DBG_NO_PSTATE_ST; wrong pixels):
+// attribute the HBM write traffic (profiles/r03/write_traffic_r03.json)
+#ifdef RT_DBG_NO_IMAGE_ST
+constexpr bool kDbgNoImage = true;
+#else
+constexpr bool kDbgNoImage = false;
+#endif
+#ifdef RT_DBG_NO_PSTATE_ST
+constexpr bool kDbgNoPathState = true;
+#else
+constexpr bool kDbgNoPathState = false;
+#endif
+#ifndef RT_PS_AUX
+#define RT_PS_AUX 0   // cache-policy bits of path-state stores (dev experiments)
+#endif
 __device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, double x) {
-  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, x), r, voff, soff, 0);
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, x), r, voff, soff, RT_PS_AUX);
 }
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 struct D2 {
@@ -243,6 +258,12 @@ struct KParams {
   int pool_off;             // LDS byte offset of the compaction pool (kPoolBytes)
   long long frame_tiles;
   const FrameDesc* frames;  // [n_frames]
+  // tile order (RT_FLAG_COST_ORDER): work item w belongs to linear tile tile_order[w / 64] instead of
+  // w / 64 (a permutation within each work head's range); tile_cost[ty * tiles_x + tx] accumulates
+  // the cost of the tile position's finished samples over the launch's frames (the next order)
+  const uint32_t* tile_order;
+  uint32_t* tile_cost;
+  int cost_time;            // tile_cost in 10-ns ticks of pixel lifetime instead of bounces
 };
 
 // ---- fp64 vector ops (course vec4 semantics on xyz) ----
@@ -375,8 +396,12 @@ __device__ __forceinline__ TriOps load_tri(const GTri* tris, uint32_t i) {
 //     fit one batch restarts from the recomputed ambient term).
 // The mirror coefficient comes from the material (the lane keeps the mesh id); the normal of
 // the bounce being shaded lives in the slot's aux words (below).
-enum : int { R_SCOLW = 0, R_PCOL = 1, R_HD = 2, R_LACC = 3, kRegions = 4 };
-constexpr uint32_t kLaneRec = 32;                 // bytes per lane and region
+//   the pixel's start time (R_COST; only with a per-tile cost map in time mode).
+enum : int { R_SCOLW = 0, R_PCOL = 1, R_HD = 2, R_LACC = 3, R_COST = 4, kRegions = 5 };
+#ifndef RT_PS_LANE_REC
+#define RT_PS_LANE_REC 32
+#endif
+constexpr uint32_t kLaneRec = RT_PS_LANE_REC;     // bytes per lane and region
 constexpr uint32_t kRegionBytes = 64 * kLaneRec;  // 2 KB per wave and region
 
 // LDS slots ([field][thread], conflict-free): the ray (the only hand-over between the
@@ -484,6 +509,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
     w = b.b;
   };
   auto ST4 = [&](int r, D3 v, double w) {
+    if (kDbgNoPathState) return;   // measurement-only build (wrong pixels): HBM writes without path state
     const uint32_t o = (uint32_t)r * kRegionBytes;
     buf_st(prs, pvo, o, v.x); buf_st(prs, pvo, o + 8u, v.y); buf_st(prs, pvo, o + 16u, v.z); buf_st(prs, pvo, o + 24u, w);
   };
@@ -585,6 +611,8 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
     // SCOL = 0 and W = 1 are implicit at depth 0, PCOL = 0 at sample 0 (never stored)
     depth = 0;
     c_primary++;
+    if (P.cost_time && P.tile_cost && sample == 0)   // the pixel's start (s_memrealtime, 100 MHz)
+      buf_st(prs, pvo, (uint32_t)R_COST * kRegionBytes, (double)(uint32_t)__builtin_amdgcn_s_memrealtime());
     emit_ray(d3(K.eye[0], K.eye[1], K.eye[2]), dir, DBL_MAX);
     state = ST_CLOSEST;
   };
@@ -632,7 +660,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
             item = wk;
           } else {
 #if RT_BAND_ORDER
-            const long long tile = wk >> 6;
+            const long long tile = P.tile_order ? (long long)P.tile_order[wk >> 6] : (wk >> 6);
             const int j = (int)(wk & 63);
             // several frames: tile row ty of every frame, then row ty + 1, so each XCD head's
             // contiguous range is a band of rows of all frames (its L2 holds one band's nodes)
@@ -1393,6 +1421,17 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
         so[0] = c.x; so[1] = c.y; so[2] = c.z;
         state = heads_left > 0 ? ST_FETCH : ST_DONE;
       } else if (finish) {
+        if (P.tile_cost) {   // cost of this sample: its bounces, or in time mode the pixel's lifetime at its
+                             // last sample, summed per tile position over the launch's frames
+          const long long t = (long long)(lrow >> 3) * P.tiles_x + (px >> 3);   // tile position (all frames)
+          uint32_t c = (uint32_t)(depth + 1);
+          if (P.cost_time) {
+            c = 0;
+            if (sample + 1 == P.spp_n * P.spp_n)
+              c = (uint32_t)__builtin_amdgcn_s_memrealtime() - (uint32_t)buf_ld(prs, pvo, (uint32_t)R_COST * kRegionBytes);
+          }
+          atomicAdd(&P.tile_cost[t], c);
+        }
         const D3 pcol = add(sample == 0 ? d3(0, 0, 0) : LDV(R_PCOL), scol);
         sample++;
         if (sample < P.spp_n * P.spp_n) {
@@ -1404,12 +1443,18 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
           const double nn = (double)n2;
           const double r = stdmin(pcol.x / nn, 1.0), g = stdmin(pcol.y / nn, 1.0), b = stdmin(pcol.z / nn, 1.0);
           const size_t o = 3 * ((size_t)lrow * P.W + px);
-          if (P.out_fmt == RT_OUT_RGB_F64) {
+          // nontemporal (evict-first): the frame is written once and never read here, so its lines
+          // should not push the path-state lines out of L2 (office: HBM writes 50.9 -> 45.5 MB per
+          // frame, time unchanged; profiles/r03/write_traffic_r03.json)
+          if (kDbgNoImage) {   // measurement-only build: HBM writes without the frame
+          } else if (P.out_fmt == RT_OUT_RGB_F64) {
             double* out = reinterpret_cast<double*>(P.frames[frame].out) + o;
-            out[0] = r; out[1] = g; out[2] = b;
+            __builtin_nontemporal_store(r, out); __builtin_nontemporal_store(g, out + 1);
+            __builtin_nontemporal_store(b, out + 2);
           } else {
             float* out = reinterpret_cast<float*>(P.frames[frame].out) + o;
-            out[0] = (float)r; out[1] = (float)g; out[2] = (float)b;
+            __builtin_nontemporal_store((float)r, out); __builtin_nontemporal_store((float)g, out + 1);
+            __builtin_nontemporal_store((float)b, out + 2);
           }
           state = heads_left > 0 ? ST_FETCH : ST_DONE;
         }
@@ -1508,6 +1553,49 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
       atomicAdd(&P.ctr[CD_BIG_LEAF_TESTS], r);
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// Cost-ordered work (RT_FLAG_COST_ORDER): each work head's range of linear tiles [n h / 8,
+// n (h + 1) / 8) is reordered so its expensive tiles come first, by the cost its tile position
+// had in the previous ordered launch (pixel lifetimes summed over that launch's frames).  The
+// launch's drain -- waves finishing the paths they started just before the queue ran dry -- is
+// then made of cheap tiles (DESIGN.md §4 "cost-ordered tiles").  One block per head range: a
+// histogram of kOrderBuckets log-spaced cost classes in LDS, a descending exclusive scan, then a
+// scatter (order within a class: arbitrary; pixels never depend on the order).
+constexpr int kOrderThreads = 1024;
+constexpr int kOrderBuckets = 128;
+__device__ __forceinline__ int cost_bucket(uint32_t c) {   // 4 classes per power of two
+  if (c == 0u) return 0;
+  const int e = 31 - __clz((int)c);
+  const int frac = e >= 2 ? (int)((c >> (e - 2)) & 3u) : (int)((c << (2 - e)) & 3u);
+  return min(kOrderBuckets - 1, 1 + e * 4 + frac);
+}
+__global__ void __launch_bounds__(kOrderThreads) tile_order_kernel(const uint32_t* cost, uint32_t* order, long long n_tiles,
+                                                                   int n_frames, int tiles_x) {
+  __shared__ uint32_t hist[kOrderBuckets];
+  const long long t0 = n_tiles * blockIdx.x / kGroups, t1 = n_tiles * (blockIdx.x + 1) / kGroups;
+  const long long row_tiles = (long long)n_frames * tiles_x;
+  auto key = [&](long long i) {   // band-major linear tile -> its position's cost class
+    const long long ty = i / row_tiles;
+    const int tx = (int)((i - ty * row_tiles) % tiles_x);
+    return cost_bucket(cost[ty * tiles_x + tx]);
+  };
+  for (int b = threadIdx.x; b < kOrderBuckets; b += kOrderThreads) hist[b] = 0u;
+  __syncthreads();
+  for (long long i = t0 + threadIdx.x; i < t1; i += kOrderThreads) atomicAdd(&hist[key(i)], 1u);
+  __syncthreads();
+  if (threadIdx.x == 0) {   // descending classes: offset of class b = tiles in classes above it
+    uint32_t run = 0;
+    for (int b = kOrderBuckets - 1; b >= 0; --b) {
+      const uint32_t c = hist[b];
+      hist[b] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+  for (long long i = t0 + threadIdx.x; i < t1; i += kOrderThreads)
+    order[t0 + atomicAdd(&hist[key(i)], 1u)] = (uint32_t)i;
 }
 
 // ---------------------------------------------------------------------------
@@ -1707,7 +1795,8 @@ size_t lds_bytes(int stack_words, int ring = kShortStack) {
 size_t lds_bytes_total(int stack_words, int n_top, int ring = kShortStack) {
   return lds_bytes(stack_words, ring) + (size_t)n_top * sizeof(GNode4) + RT_MAX_LIGHTS * 6 * sizeof(double) + kPoolBytes;
 }
-// treelet nodes that fit next to a ring of the given size in a block's 40 KB
+// treelet nodes that fit next to a ring of the given size in a block's 40 KB (kTopNodes beside the
+// 8-entry ring)
 int top_nodes_for(int stack_words, int ring, int n_gnodes4) {
   const long long room = 40960 - (long long)lds_bytes_total(stack_words, 0, ring);
   return (int)std::max(0LL, std::min<long long>({room / (long long)sizeof(GNode4), (long long)kTopNodes, (long long)n_gnodes4}));
@@ -1762,18 +1851,27 @@ struct rt_scene {
   double root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};
   long long bytes = 0;
   int n_cu = 0;
-  int blocks_per_cu[kNumVariants] = {0, 0, 0, 0, 0};
+  int blocks_per_cu[kNumVariants] = {};
   bool deep = false;            // launches use the 16-entry ring variant (deep hierarchy)
-  int n_top_deep = 0;           // treelet nodes beside the 16-entry ring
+  int n_top_v[kNumVariants] = {};   // treelet nodes of each kernel variant (by its stack ring)
   GNode4* d_nodes4 = nullptr;
   int n_gnodes4 = 0;
-  int n_top = 0;                // 4-wide nodes each block caches in LDS
   int bpc_cap = 0;              // rt_upload_options.blocks_per_cu (0: as many as fit)
   int grid_spare = 0;           // rt_upload_options.grid_spare
   std::vector<GMat> mesh_mats;  // host copy: the analytic materials are appended after these
   GPrim* d_prims = nullptr;     // analytic primitives (rt_scene_set_analytic), spheres then planes
   int n_prims = 0;
   long long table_bytes = 0;    // device bytes of d_mats + d_prims
+  // per-tile-position cost maps (RT_FLAG_COST_ORDER / RT_FLAG_TILE_COST*): the last launch wrote
+  // d_cost[cost_cur] (cost_n positions, tiles_x wide; valid for that geometry)
+  uint32_t* d_cost[2] = {nullptr, nullptr};
+  long long cost_cap = 0, cost_n = 0;
+  int cost_tiles_x = 0, cost_cur = 0;
+  bool cost_valid = false;
+  uint32_t* d_order = nullptr;        // RT_FLAG_COST_ORDER: this launch's tile order
+  long long order_cap = 0;
+  uint32_t* d_tile_order = nullptr;  // rt_debug_set_tile_order: work order of launches with that many tiles
+  long long tile_order_n = 0;
 };
 
 namespace {
@@ -1844,15 +1942,16 @@ int upload_image(const SceneImage& I, const rt_upload_options& opt, int device, 
   sc->depth = I.depth;
   sc->stack_words = std::max(std::max(1, I.depth), I.stack4);
   sc->n_gnodes4 = (int)I.nodes4.size();
-  sc->n_top = RT_TOP_NODES > 0 ? std::min(kTopNodes, sc->n_gnodes4) : 0;
-  if (opt.lds_treelet >= 0) sc->n_top = std::min(sc->n_top, opt.lds_treelet);   // cache fewer nodes (0 = none)
   // deep hierarchies (half a million device records and more: random-triangle soups of ~1 M and
   // up spill an 8-entry ring on every other ray, the office proxy on 1 in 130) render with the
   // 16-entry ring and the 9-node treelet that fits beside it (A/B)
   sc->deep = I.tris.size() >= (size_t)(1u << 18);   // device records (office 77 k prefers 8, 500 k random 16)
   if (opt.stack_ring != 0) sc->deep = opt.stack_ring >= 16;   // forced ring size
-  sc->n_top_deep = RT_TOP_NODES > 0 ? top_nodes_for(sc->stack_words, kRingDeep, sc->n_gnodes4) : 0;
-  if (opt.lds_treelet >= 0) sc->n_top_deep = std::min(sc->n_top_deep, opt.lds_treelet);
+  for (int v = 0; v < kNumVariants; ++v) {
+    int& nt = sc->n_top_v[v];
+    nt = RT_TOP_NODES > 0 ? top_nodes_for(sc->stack_words, variant_ring(v), sc->n_gnodes4) : 0;
+    if (opt.lds_treelet >= 0) nt = std::min(nt, opt.lds_treelet);   // cache fewer nodes (0 = none)
+  }
   sc->bpc_cap = opt.blocks_per_cu;
   sc->grid_spare = opt.grid_spare;
   sc->delta = I.delta;
@@ -1867,7 +1966,7 @@ int upload_image(const SceneImage& I, const rt_upload_options& opt, int device, 
   int max_blocks = 1;
   for (int v = 0; v < kNumVariants; ++v) {
     const int ring = variant_ring(v);
-    const size_t lds = lds_bytes_total(sc->stack_words, ring == kRingDeep ? sc->n_top_deep : sc->n_top, ring);
+    const size_t lds = lds_bytes_total(sc->stack_words, sc->n_top_v[v], ring);
     int nb = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(kVariants[v].fn), kBlock, lds) !=
             hipSuccess || nb < 1)
@@ -2110,13 +2209,57 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   P.list = list;
   P.list_count = count;
   P.sample_out = sample_out;
+  if (!list && sc->d_tile_order && sc->tile_order_n == P.n_tiles) P.tile_order = sc->d_tile_order;
+  // cost-ordered work: this launch is ordered by the previous cost map of the same geometry and
+  // writes the next one (DESIGN.md §4 "cost-ordered tiles")
+  const bool cost_order = !list && (p->flags & RT_FLAG_COST_ORDER);
+  const bool want_cost = cost_order || (!list && (p->flags & (RT_FLAG_TILE_COST | RT_FLAG_TILE_COST_TIME)));
+  int cost_next = -1;
+  if (want_cost) {
+    const long long n_pos = (long long)P.tiles_x * ((rows + 7) / 8);
+    if (sc->cost_cap < n_pos) {
+      HIP_TRY(hipDeviceSynchronize());   // launches in flight may still use the old maps
+      for (int k = 0; k < 2; ++k) {
+        if (sc->d_cost[k]) HIP_TRY(hipFree(sc->d_cost[k]));
+        sc->d_cost[k] = nullptr;
+      }
+      sc->cost_cap = 0;
+      sc->cost_valid = false;
+      for (int k = 0; k < 2; ++k)
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&sc->d_cost[k]), (size_t)n_pos * sizeof(uint32_t)));
+      sc->cost_cap = n_pos;
+    }
+    if (sc->cost_n != n_pos || sc->cost_tiles_x != P.tiles_x) sc->cost_valid = false;   // other geometry
+    if (sc->last_ctx >= 0)   // the previous launch (any stream) has finished writing / reading the maps
+      HIP_TRY(hipStreamWaitEvent(st, sc->ctx[sc->last_ctx].ev1, 0));
+    if (cost_order && sc->cost_valid) {
+      if (sc->order_cap < P.n_tiles) {
+        HIP_TRY(hipDeviceSynchronize());
+        if (sc->d_order) HIP_TRY(hipFree(sc->d_order));
+        sc->d_order = nullptr;
+        sc->order_cap = 0;
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&sc->d_order), (size_t)P.n_tiles * sizeof(uint32_t)));
+        sc->order_cap = P.n_tiles;
+      }
+      hipLaunchKernelGGL(tile_order_kernel, dim3(kGroups), dim3(kOrderThreads), 0, st,
+                         (const uint32_t*)sc->d_cost[sc->cost_cur], sc->d_order, P.n_tiles, n_frames, P.tiles_x);
+      HIP_TRY(hipGetLastError());
+      P.tile_order = sc->d_order;
+    }
+    cost_next = sc->cost_valid ? sc->cost_cur ^ 1 : sc->cost_cur;
+    HIP_TRY(hipMemsetAsync(sc->d_cost[cost_next], 0, (size_t)n_pos * sizeof(uint32_t), st));
+    P.tile_cost = sc->d_cost[cost_next];
+    P.cost_time = (p->flags & (RT_FLAG_TILE_COST_TIME | RT_FLAG_COST_ORDER)) ? 1 : 0;
+    sc->cost_n = n_pos;
+    sc->cost_tiles_x = P.tiles_x;
+  }
 
   const int v = (p->flags & RT_FLAG_TRAVERSAL_STATS) ? 2
                 : (p->flags & RT_FLAG_WIDE_STATS) ? 1
                 : (p->flags & RT_FLAG_TIMELINE) ? 3
                 : sc->deep ? 4 : 0;   // 4: the 16-entry-ring production variant
   const int ring = variant_ring(v);
-  const int n_top = ring == kRingDeep ? sc->n_top_deep : sc->n_top;
+  const int n_top = sc->n_top_v[v];
   const size_t lds = lds_bytes_total(sc->stack_words, n_top, ring);
   P.n_top = n_top;
   P.top_off = (int)lds_bytes(sc->stack_words, ring);
@@ -2163,6 +2306,10 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
                             args, lds, st));
   }
   HIP_TRY(hipEventRecord(C.ev1, st));
+  if (cost_next >= 0) {   // this launch's costs order the next ordered launch of this geometry
+    sc->cost_cur = cost_next;
+    sc->cost_valid = true;
+  }
   C.used = true;
   C.variant = v;
   C.waves = rows > 0 ? blocks * (kBlock / 64) : 0;
@@ -2421,6 +2568,35 @@ int rt_debug_blocks_per_cu(rt_scene* sc, int variant) {
   return sc->blocks_per_cu[variant];
 }
 
+long long rt_debug_tile_cost(rt_scene* sc, unsigned int* out, long long n) {
+  if (!sc) return fail(RT_ERR_INVALID, "rt_debug_tile_cost: null scene");
+  if (!sc->cost_valid) return 0;
+  if (hipSetDevice(sc->device) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+    return fail(RT_ERR_HIP, "rt_debug_tile_cost: synchronize failed");
+  const long long m = std::min(n, sc->cost_n);
+  if (out && m > 0 &&
+      hipMemcpy(out, sc->d_cost[sc->cost_cur], (size_t)m * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
+    return fail(RT_ERR_HIP, "rt_debug_tile_cost: copy failed");
+  return sc->cost_n;
+}
+
+int rt_debug_set_tile_order(rt_scene* sc, const unsigned int* order, long long n) {
+  if (!sc || n < 0 || (n > 0 && !order)) return fail(RT_ERR_INVALID, "rt_debug_set_tile_order: bad argument");
+  if (hipSetDevice(sc->device) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+    return fail(RT_ERR_HIP, "rt_debug_set_tile_order: synchronize failed");
+  for (long long i = 0; i < n; ++i)
+    if ((long long)order[i] >= n) return fail(RT_ERR_INVALID, "rt_debug_set_tile_order: not a permutation");
+  if (sc->d_tile_order) (void)hipFree(sc->d_tile_order);
+  sc->d_tile_order = nullptr;
+  sc->tile_order_n = 0;
+  if (n == 0) return RT_OK;
+  if (hipMalloc(reinterpret_cast<void**>(&sc->d_tile_order), (size_t)n * sizeof(uint32_t)) != hipSuccess ||
+      hipMemcpy(sc->d_tile_order, order, (size_t)n * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess)
+    return fail(RT_ERR_HIP, "rt_debug_set_tile_order: upload failed");
+  sc->tile_order_n = n;
+  return RT_OK;
+}
+
 long long rt_debug_timeline(rt_scene* sc, unsigned long long* out, long long n) {
   if (!sc || !out || n <= 0) return fail(RT_ERR_INVALID, "rt_debug_timeline: bad argument");
   HIP_TRY(hipSetDevice(sc->device));
@@ -2520,7 +2696,7 @@ void rt_scene_free(rt_scene* sc) {
   if (!sc) return;
   (void)hipSetDevice(sc->device);
   (void)hipDeviceSynchronize();   // launches may still be reading the scene
-  void* ptrs[] = {sc->d_nodes, sc->d_nodes4, sc->d_tris, sc->d_shade, sc->d_tnorm, sc->d_tu,
+  void* ptrs[] = {sc->d_cost[0], sc->d_cost[1], sc->d_order, sc->d_tile_order, sc->d_nodes, sc->d_nodes4, sc->d_tris, sc->d_shade, sc->d_tnorm, sc->d_tu,
                   sc->d_tv, sc->d_texels, sc->d_mats, sc->d_lights, sc->d_slot2dev, sc->d_prims};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);

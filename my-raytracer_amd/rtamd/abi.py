@@ -21,6 +21,9 @@ RT_OUT_RGB_F64 = 1
 RT_FLAG_TRAVERSAL_STATS = 1
 RT_FLAG_WIDE_STATS = 2
 RT_FLAG_TIMELINE = 4
+RT_FLAG_TILE_COST = 8
+RT_FLAG_TILE_COST_TIME = 16
+RT_FLAG_COST_ORDER = 32
 
 
 class Material(C.Structure):
@@ -174,6 +177,8 @@ HIP_SYMBOLS = {
     "rt_debug_counters": (C.c_int, [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]),
     "rt_debug_wave_log": (C.c_longlong, [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_longlong]),
     "rt_debug_timeline": (C.c_longlong, [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_longlong]),
+    "rt_debug_tile_cost": (C.c_longlong, [C.c_void_p, C.POINTER(C.c_uint), C.c_longlong]),
+    "rt_debug_set_tile_order": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint), C.c_longlong]),
     "rt_debug_blocks_per_cu": (C.c_int, [C.c_void_p, C.c_int]),
     "rt_scene_free": (None, [C.c_void_p]),
     "rt_last_error": (C.c_char_p, []),

@@ -204,6 +204,47 @@ def test_deterministic_and_stream_launch():
     assert dev.last_kernel_ms() > 0
 
 
+@pytest.mark.parametrize("nf", [1, 3])
+def test_tile_order_and_costs_change_no_pixel(nf):
+    # Work order (rt_debug_set_tile_order: any permutation of the launch's tiles) and the per-tile
+    # cost maps (RT_FLAG_TILE_COST / _TIME) change neither pixels nor ray counts.
+    import ctypes as C
+    import torch
+
+    hs, dev, _ = Case.get("office")
+    lib = rtamd.hip_lib()
+    base = hs.render_params(200, 113, 1)
+    cams = [rtamd.camera_orbit(base, 0.05 * f) for f in range(nf)]
+    outs = [torch.zeros((113, 200, 3), dtype=torch.float32, device="cuda") for _ in range(nf)]
+
+    def render(flags=0):
+        ps = [rtamd.abi.RenderParams.from_buffer_copy(c) for c in cams]
+        for q in ps:
+            q.flags = flags
+        st = dev.launch_frames(ps, [o.data_ptr() for o in outs], stats=True)
+        return [o.cpu().numpy().copy() for o in outs], counts(st)
+
+    ref, rc = render()
+    n_tiles = 25 * 15 * nf
+    for flag in (rtamd.abi.RT_FLAG_TILE_COST, rtamd.abi.RT_FLAG_TILE_COST_TIME, rtamd.abi.RT_FLAG_COST_ORDER,
+                 rtamd.abi.RT_FLAG_COST_ORDER):   # (the second ordered launch follows the first one's costs)
+        img, c = render(flag)
+        assert all(np.array_equal(a, b) for a, b in zip(img, ref)) and c == rc
+        n = lib.rt_debug_tile_cost(dev._h, None, 0)
+        assert n == 25 * 15   # tile positions (summed over the frames)
+        cost = np.zeros(n, dtype=np.uint32)
+        lib.rt_debug_tile_cost(dev._h, cost.ctypes.data_as(C.POINTER(C.c_uint)), n)
+        assert cost.min() > 0
+    order = np.random.default_rng(5).permutation(n_tiles).astype(np.uint32)
+    assert lib.rt_debug_set_tile_order(dev._h, order.ctypes.data_as(C.POINTER(C.c_uint)), n_tiles) == 0
+    img, c = render()
+    assert all(np.array_equal(a, b) for a, b in zip(img, ref)) and c == rc
+    bad = order.copy()
+    bad[0] = n_tiles
+    assert lib.rt_debug_set_tile_order(dev._h, bad.ctypes.data_as(C.POINTER(C.c_uint)), n_tiles) != 0
+    assert lib.rt_debug_set_tile_order(dev._h, None, 0) == 0
+
+
 def test_concurrent_launches_on_streams_are_independent():
     # Frames in flight on several streams use separate launch contexts (path state,
     # work heads): each result equals its serial render, bit for bit, also when more
