@@ -14,8 +14,10 @@ next launch) by ONE launch of the persistent kernel (rt_launch_frames: the frame
 work queue, so the drain at the end of a launch is paid once per F frames).  The
 F frames of a launch follow an animation path (rtamd.camera_orbit, --sweep): they
 are distinct views, and every frame traces all of its rays.  A single_frame record
-(one frame per launch, the reference's use, mytracer_gpu.cu:59-81) is timed after
-the main run.  --streams S > 1 keeps S launches in flight on separate streams
+(one frame per launch, the reference's use, mytracer_gpu.cu:59-81; consecutive views of
+the orbit) is timed after the main run, and beside it single_frame.cost_ordered: the same
+launches with RT_FLAG_COST_ORDER (each launch's work heads take the tiles that took
+longest in the previous launch first, shortening the drain).  --streams S > 1 keeps S launches in flight on separate streams
 (default 1 on one GPU: launches serial, so the HIP-event launch duration is the
 kernel's own duration, as rocprofv3 reports it; 2 on N > 1, so the RCCL gather of
 launch i overlaps launch i+1).
@@ -219,8 +221,9 @@ def main():
     n_full, rem = divmod(a.steps, F)
     st = launch_counts(F)
     rays_timed_local = n_full * rays_of(st) + (rays_of(launch_counts(rem)) if rem else 0)
-    st1 = launch_counts(1)                               # frame 0 alone: the single-frame record
-    rays_frame0_local = rays_of(st1)
+    # the single-frame records render frames cams[0 .. NS) one per launch (an animation: distinct views)
+    NS = max(1, min(a.single_frames, F))
+    rays_frame0_local = rays_of(launch_counts(NS)) / NS  # rays per frame of those frames
     tst = launch_counts(F, rtamd.RT_FLAG_TRAVERSAL_STATS)   # canonical 2-wide walk of the reference tree
     wst = launch_counts(F, rtamd.RT_FLAG_WIDE_STATS)        # the production kernel's own fetches
     adaptive_info = None
@@ -248,8 +251,9 @@ def main():
 
     starts, ends, launch_frames = [], [], []
 
-    def launch(li, nf, timed):
-        """Launch li renders nf frames (steps); their stripes are then gathered to rank 0."""
+    def launch(li, nf, timed, flags=0):
+        """Launch li renders nf frames (steps); their stripes are then gathered to rank 0.  A one-frame
+        launch renders view cams[li % F] (the single-frame records: consecutive frames of the orbit)."""
         nonlocal image
         s = streams[li % S]
         bs = [fbufs[li % S][f] for f in range(nf)]
@@ -263,7 +267,11 @@ def main():
                 gpu.launch(p64s[0], prims[li % S][0].data_ptr(), stats=False, stream=s.cuda_stream)
                 adaptive_pass(prims[li % S][0], bs[0], False, s.cuda_stream)
             elif nf == 1:
-                gpu.launch(cams[0], bs[0].data_ptr(), stats=False, stream=s.cuda_stream)
+                c1 = cams[li % len(cams)]
+                if flags:
+                    c1 = rtamd.abi.RenderParams.from_buffer_copy(c1)
+                    c1.flags = flags
+                gpu.launch(c1, bs[0].data_ptr(), stats=False, stream=s.cuda_stream)
             else:
                 gpu.launch_frames(cams[:nf], [b.data_ptr() for b in bs], stats=False, stream=s.cuda_stream)
             if timed:
@@ -274,11 +282,11 @@ def main():
             # N>1: ONE RCCL gather of the nf frames' stripes + re-interleave
             image = gathers[li % S](fbufs[li % S][:nf])
 
-    def run(steps, timed, per_launch=F):
+    def run(steps, timed, per_launch=F, flags=0):
         li, done = 0, 0
         while done < steps:
             nf = min(per_launch, steps - done)
-            launch(li, nf, timed)
+            launch(li, nf, timed, flags)
             li += 1
             done += nf
 
@@ -305,13 +313,19 @@ def main():
     last_image = image
 
     # single-frame record: the reference's use, one frame per launch (mytracer_gpu.cu:59-81)
+    # (NS consecutive views of the orbit, one per launch), then the same with RT_FLAG_COST_ORDER: each
+    # launch ordered by the previous launch's per-tile costs (one ordered pass of the NS views first)
     single = None
     if a.single_frames > 0 and not a.adaptive:
-        starts.clear(); ends.clear(); launch_frames.clear()
-        single_elapsed = timed_region(lambda: run(a.single_frames, True, per_launch=1))
-        single = {"frames": a.single_frames, "rays_per_frame": None,
-                  "ms_per_frame": round(single_elapsed / a.single_frames * 1e3, 4),
-                  "kernel_ms_avg": round(float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)])), 4)}
+        def single_record(flags):
+            starts.clear(); ends.clear(); launch_frames.clear()
+            el = timed_region(lambda: run(NS, True, per_launch=1, flags=flags))
+            return {"frames": NS, "rays_per_frame": None, "ms_per_frame": round(el / NS * 1e3, 4),
+                    "kernel_ms_avg": round(float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)])), 4)}
+        single = single_record(0)
+        run(NS, False, per_launch=1, flags=rtamd.abi.RT_FLAG_COST_ORDER)
+        single["cost_ordered"] = single_record(rtamd.abi.RT_FLAG_COST_ORDER)
+        single["views"] = "consecutive camera-orbit views, one per launch"
 
     tot = torch.tensor([rays_timed_local, rays_frame0_local, work_bytes_frame], dtype=torch.float64, device="cuda")
     if n > 1:
@@ -325,9 +339,10 @@ def main():
         ms_per_step = elapsed / a.steps * 1e3
         mrays = rays_total / elapsed / 1e6
         if single is not None:
-            single["rays_per_frame"] = int(rays_frame0)
-            single["value"] = round(rays_frame0 / (single["ms_per_frame"] * 1e-3) / 1e6, 2)
-            single["unit"] = "Mrays/s"
+            for rec in (single, single["cost_ordered"]):
+                rec["rays_per_frame"] = int(rays_frame0)
+                rec["value"] = round(rays_frame0 / (rec["ms_per_frame"] * 1e-3) / 1e6, 2)
+                rec["unit"] = "Mrays/s"
         pmc = pmc_per_frame(workload_key(a, n), frames_per_launch)
         kernel_s = kernel_ms_avg * 1e-3
         roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": None,
@@ -397,7 +412,7 @@ def main():
                 "host_bvh_build_s": round(build_s, 4),
                 # frames the production kernel rendered in this process (counting launches, warm-up,
                 # timed run, single-frame run): the divisor tools/pmc_summary.py uses for per-frame bytes
-                "production_frames_rendered": (F + rem + 1 + a.warmup + a.steps + (a.single_frames if single else 0)
+                "production_frames_rendered": (F + rem + 1 + a.warmup + a.steps + (3 * NS if single else 0)
                                                if not a.adaptive else None),
                 "device_scene_MB": round(gpu.device_bytes / 1e6, 1),
                 **({"upload_options": upload_opts} if upload_opts else {}),

@@ -102,10 +102,12 @@ enum {
   RT_FLAG_TIMELINE = 4,        /* production kernel + per-round timeline (diagnostics, rt_debug_timeline) */
   RT_FLAG_TILE_COST = 8,       /* diagnostics: per-tile cost of the launch (rt_debug_tile_cost): bounces */
   RT_FLAG_TILE_COST_TIME = 16, /* ... the same, as pixel lifetimes (10-ns ticks) */
-  RT_FLAG_COST_ORDER = 32      /* work order: every work head renders the tiles that cost most in the previous
-                                  RT_FLAG_COST_ORDER launch of the same image geometry first (animation: frame
-                                  i's costs order frame i + 1), and this launch's costs are kept for the next;
-                                  shortens the end-of-launch drain; pixels are unchanged */
+  RT_FLAG_COST_ORDER = 32      /* one-frame launches (the reference's use): every work head renders the tiles
+                                  that took longest in the previous RT_FLAG_COST_ORDER launch of the same image
+                                  geometry first (animation: frame i's costs order frame i + 1), and this
+                                  launch's costs are kept for the next; shortens the end-of-launch drain.
+                                  Launches of several frames, or of more than 32768 tiles, keep the natural
+                                  order but still record costs.  Pixels are unchanged */
 };
 
 /* One render call.  Rows are rendered as interleaved stripes:
@@ -345,6 +347,9 @@ long long rt_debug_tile_cost(rt_scene* scene, unsigned int* out, long long n);
 /* Diagnostics: launches with exactly n tiles take linear tile order[w / 64] for work item w (a
  * permutation; pixels do not depend on it); n = 0 clears. */
 int rt_debug_set_tile_order(rt_scene* scene, const unsigned int* order, long long n);
+/* Diagnostics: the tile order the last RT_FLAG_COST_ORDER launch used (order[i] = tile rendered i-th
+ * within its work head's range) into out[0..n); returns its length, 0 if none. */
+long long rt_debug_last_tile_order(rt_scene* scene, unsigned int* out, long long n);
 
 void rt_scene_free(rt_scene* scene);
 

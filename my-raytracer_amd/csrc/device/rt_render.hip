@@ -47,6 +47,8 @@
 #include <thread>
 #include <vector>
 
+#include <rocprim/block/block_radix_sort.hpp>
+
 #include "../../../include/rt_hip.h"
 #include "../host/device_image.hpp"
 #include "rt_layout.hpp"
@@ -396,8 +398,7 @@ __device__ __forceinline__ TriOps load_tri(const GTri* tris, uint32_t i) {
 //     fit one batch restarts from the recomputed ambient term).
 // The mirror coefficient comes from the material (the lane keeps the mesh id); the normal of
 // the bounce being shaded lives in the slot's aux words (below).
-//   the pixel's start time (R_COST; only with a per-tile cost map in time mode).
-enum : int { R_SCOLW = 0, R_PCOL = 1, R_HD = 2, R_LACC = 3, R_COST = 4, kRegions = 5 };
+enum : int { R_SCOLW = 0, R_PCOL = 1, R_HD = 2, R_LACC = 3, kRegions = 4 };
 #ifndef RT_PS_LANE_REC
 #define RT_PS_LANE_REC 32
 #endif
@@ -434,6 +435,7 @@ __device__ __forceinline__ float f4c(const float4& v, int c) {
 __device__ __forceinline__ uint32_t u4c(const uint4& v, int c) {
   return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
 }
+
 
 #ifndef RT_WAVES_PER_EU
 #define RT_WAVES_PER_EU 4   // 4 waves/SIMD = 16 waves/CU (register budget 128 VGPRs)
@@ -533,6 +535,8 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
   int state = ST_FETCH;
   int px = 0, lrow = 0, py = 0, sample = 0, depth = 0, light = 0, mesh = 0, frame = 0;
   long long item = 0;       // list mode: work item (pixel * nsamp + sample), may exceed 2^31
+  uint32_t pix_t0 = 0;      // start of the pixel (s_memrealtime; cost maps in time mode.  A pixel handed
+                            // over by tail compaction restarts it at its adoption)
   int best = kNoHit;        // device record of the closest hit
   int best_slot = kNoHit;   // its reference slot (tie-break key)
   double thit = DBL_MAX;
@@ -611,8 +615,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
     // SCOL = 0 and W = 1 are implicit at depth 0, PCOL = 0 at sample 0 (never stored)
     depth = 0;
     c_primary++;
-    if (P.cost_time && P.tile_cost && sample == 0)   // the pixel's start (s_memrealtime, 100 MHz)
-      buf_st(prs, pvo, (uint32_t)R_COST * kRegionBytes, (double)(uint32_t)__builtin_amdgcn_s_memrealtime());
+    if (sample == 0) pix_t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();   // the pixel's start (100 MHz)
     emit_ray(d3(K.eye[0], K.eye[1], K.eye[2]), dir, DBL_MAX);
     state = ST_CLOSEST;
   };
@@ -1001,20 +1004,26 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
             fz = *reinterpret_cast<const float4*>(lb + (nzo ^ 16u));
             rf = *reinterpret_cast<const uint4*>(lb + 96);
           } else {
-            const char* nb = reinterpret_cast<const char*>(P.nodes4) + (size_t)cur * sizeof(GNode4);
+            // 32-bit byte offsets from the node array's base (an SGPR pair): global_load's saddr
+            // form, one 32-bit OR per plane instead of 64-bit address arithmetic (office +0.7 %,
+            // config 4 +1.1 %; the node array stays below 4 GB: checked at upload)
+            const char* nbase = reinterpret_cast<const char*>(P.nodes4);
+            const uint32_t nbo = cur * (uint32_t)sizeof(GNode4);
+#define RT_NODE_AT(off) (nbase + (uint32_t)(nbo + (off)))
             if constexpr (TL) { tl_gnode++; tl_wave_gap(1); }
             if (STATS) {
               wave_distinct(cur, d_gn_dist, lane);
               const uint32_t c0 = __shfl(cur, __ffsll((long long)__ballot(1)) - 1);
               if (__ballot(cur != c0) == 0) wave_tick(d_gn_uni, d_dummy, lane);
             }
-            nx = *reinterpret_cast<const float4*>(nb + nxo);
-            fx = *reinterpret_cast<const float4*>(nb + (nxo ^ 16u));
-            ny = *reinterpret_cast<const float4*>(nb + nyo);
-            fy = *reinterpret_cast<const float4*>(nb + (nyo ^ 16u));
-            nz = *reinterpret_cast<const float4*>(nb + nzo);
-            fz = *reinterpret_cast<const float4*>(nb + (nzo ^ 16u));
-            rf = *reinterpret_cast<const uint4*>(nb + 96);
+            nx = *reinterpret_cast<const float4*>(RT_NODE_AT(nxo));
+            fx = *reinterpret_cast<const float4*>(RT_NODE_AT(nxo ^ 16u));
+            ny = *reinterpret_cast<const float4*>(RT_NODE_AT(nyo));
+            fy = *reinterpret_cast<const float4*>(RT_NODE_AT(nyo ^ 16u));
+            nz = *reinterpret_cast<const float4*>(RT_NODE_AT(nzo));
+            fz = *reinterpret_cast<const float4*>(RT_NODE_AT(nzo ^ 16u));
+            rf = *reinterpret_cast<const uint4*>(RT_NODE_AT(96u));
+#undef RT_NODE_AT
           }
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
@@ -1225,6 +1234,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
 #pragma unroll
             for (int k = 0; k < kSlotDoubles; ++k) lds_d[k * kBlock + threadIdx.x] = lds_d[k * kBlock + t];
             thit = *R.tlim;   // a closest-hit ray's distance (a shadow batch's owner does not read thit)
+            pix_t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
           }
           I &= ~__ballot(take);
         }
@@ -1428,9 +1438,22 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
           if (P.cost_time) {
             c = 0;
             if (sample + 1 == P.spp_n * P.spp_n)
-              c = (uint32_t)__builtin_amdgcn_s_memrealtime() - (uint32_t)buf_ld(prs, pvo, (uint32_t)R_COST * kRegionBytes);
+              c = (uint32_t)__builtin_amdgcn_s_memrealtime() - pix_t0;
           }
-          atomicAdd(&P.tile_cost[t], c);
+          // one atomic per distinct tile among the lanes finishing here (a wave's lanes mostly share
+          // one or two tiles; 64 atomics on one address queue at the memory side)
+          unsigned long long m = __ballot(1);
+          while (m != 0ull) {
+            const int ld = __ffsll((long long)m) - 1;
+            const uint32_t tl = (uint32_t)__shfl((int)t, ld);
+            const bool same = (uint32_t)t == tl;
+            const unsigned long long ms = __ballot(same);
+            uint32_t sum = same ? c : 0u;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) sum += (uint32_t)__shfl_xor((int)sum, o);
+            if (lane == ld) atomicAdd(&P.tile_cost[tl], sum);
+            m &= ~ms;
+          }
         }
         const D3 pcol = add(sample == 0 ? d3(0, 0, 0) : LDV(R_PCOL), scol);
         sample++;
@@ -1556,46 +1579,42 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
 }
 
 // ---------------------------------------------------------------------------
-// Cost-ordered work (RT_FLAG_COST_ORDER): each work head's range of linear tiles [n h / 8,
-// n (h + 1) / 8) is reordered so its expensive tiles come first, by the cost its tile position
-// had in the previous ordered launch (pixel lifetimes summed over that launch's frames).  The
+// Cost-ordered work (RT_FLAG_COST_ORDER, one-frame launches): each work head's range of tiles
+// [n h / 8, n (h + 1) / 8) is reordered so its expensive tiles come first, by the cost its tile
+// position had in the previous ordered launch (pixel lifetimes, 10-ns ticks).  A one-frame
 // launch's drain -- waves finishing the paths they started just before the queue ran dry -- is
-// then made of cheap tiles (DESIGN.md §4 "cost-ordered tiles").  One block per head range: a
-// histogram of kOrderBuckets log-spaced cost classes in LDS, a descending exclusive scan, then a
-// scatter (order within a class: arbitrary; pixels never depend on the order).
+// then made of cheap tiles: office 1080p 0.570 -> 0.450 ms with an exact order (tools/
+// order_probe.py; DESIGN.md §4 "cost-ordered tiles").  One block per head range sorts keys
+// (cost descending, then tile index: the order is exact and, among equal costs, spatial) with a
+// block radix sort; the block also zeroes the next cost map.
 constexpr int kOrderThreads = 1024;
-constexpr int kOrderBuckets = 128;
-__device__ __forceinline__ int cost_bucket(uint32_t c) {   // 4 classes per power of two
-  if (c == 0u) return 0;
-  const int e = 31 - __clz((int)c);
-  const int frac = e >= 2 ? (int)((c >> (e - 2)) & 3u) : (int)((c << (2 - e)) & 3u);
-  return min(kOrderBuckets - 1, 1 + e * 4 + frac);
-}
+constexpr int kOrderItems = 4;
+constexpr long long kOrderMaxRange = (long long)kOrderThreads * kOrderItems;   // tiles per head range
 __global__ void __launch_bounds__(kOrderThreads) tile_order_kernel(const uint32_t* cost, uint32_t* order, long long n_tiles,
-                                                                   int n_frames, int tiles_x) {
-  __shared__ uint32_t hist[kOrderBuckets];
+                                                                   uint32_t* next_cost, long long n_next) {
+  using Sort = rocprim::block_radix_sort<unsigned int, kOrderThreads, kOrderItems>;
+  __shared__ typename Sort::storage_type storage;
   const long long t0 = n_tiles * blockIdx.x / kGroups, t1 = n_tiles * (blockIdx.x + 1) / kGroups;
-  const long long row_tiles = (long long)n_frames * tiles_x;
-  auto key = [&](long long i) {   // band-major linear tile -> its position's cost class
-    const long long ty = i / row_tiles;
-    const int tx = (int)((i - ty * row_tiles) % tiles_x);
-    return cost_bucket(cost[ty * tiles_x + tx]);
-  };
-  for (int b = threadIdx.x; b < kOrderBuckets; b += kOrderThreads) hist[b] = 0u;
-  __syncthreads();
-  for (long long i = t0 + threadIdx.x; i < t1; i += kOrderThreads) atomicAdd(&hist[key(i)], 1u);
-  __syncthreads();
-  if (threadIdx.x == 0) {   // descending classes: offset of class b = tiles in classes above it
-    uint32_t run = 0;
-    for (int b = kOrderBuckets - 1; b >= 0; --b) {
-      const uint32_t c = hist[b];
-      hist[b] = run;
-      run += c;
+  unsigned int keys[kOrderItems];
+#pragma unroll
+  for (int j = 0; j < kOrderItems; ++j) {
+    const long long li = (long long)threadIdx.x * kOrderItems + j;   // local index in the range
+    keys[j] = 0xffffffffu;                                          // padding sorts last
+    if (t0 + li < t1) {
+      // fp32 bits of the cost: monotonic for costs >= 0; 20 bits (8 exponent + 12 mantissa bits)
+      // inverted so that higher costs sort first, then the 12-bit local index
+      const uint32_t q = __float_as_uint((float)cost[t0 + li]) >> 11;
+      keys[j] = ((0xfffffu - q) << 12) | (uint32_t)li;
     }
   }
-  __syncthreads();
-  for (long long i = t0 + threadIdx.x; i < t1; i += kOrderThreads)
-    order[t0 + atomicAdd(&hist[key(i)], 1u)] = (uint32_t)i;
+  Sort().sort(keys, storage);
+#pragma unroll
+  for (int j = 0; j < kOrderItems; ++j) {
+    const long long pos = (long long)threadIdx.x * kOrderItems + j;
+    if (t0 + pos < t1) order[t0 + pos] = (uint32_t)(t0 + (keys[j] & 0xfffu));
+  }
+  for (long long i = (long long)blockIdx.x * kOrderThreads + threadIdx.x; i < n_next; i += (long long)kGroups * kOrderThreads)
+    next_cost[i] = 0u;
 }
 
 // ---------------------------------------------------------------------------
@@ -1870,6 +1889,7 @@ struct rt_scene {
   bool cost_valid = false;
   uint32_t* d_order = nullptr;        // RT_FLAG_COST_ORDER: this launch's tile order
   long long order_cap = 0;
+  long long last_order_n = 0;         // tiles of the last ordered launch (rt_debug_last_tile_order)
   uint32_t* d_tile_order = nullptr;  // rt_debug_set_tile_order: work order of launches with that many tiles
   long long tile_order_n = 0;
 };
@@ -1942,6 +1962,10 @@ int upload_image(const SceneImage& I, const rt_upload_options& opt, int device, 
   sc->depth = I.depth;
   sc->stack_words = std::max(std::max(1, I.depth), I.stack4);
   sc->n_gnodes4 = (int)I.nodes4.size();
+  if ((unsigned long long)I.nodes4.size() * sizeof(GNode4) >= (1ull << 32)) {   // 32-bit node offsets
+    rt_scene_free(sc);
+    return fail(RT_ERR_UNSUPPORTED, "rt_scene_upload: more than 2^25 4-wide nodes");
+  }
   // deep hierarchies (half a million device records and more: random-triangle soups of ~1 M and
   // up spill an 8-entry ring on every other ray, the office proxy on 1 in 130) render with the
   // 16-entry ring and the 9-node treelet that fits beside it (A/B)
@@ -2212,7 +2236,9 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   if (!list && sc->d_tile_order && sc->tile_order_n == P.n_tiles) P.tile_order = sc->d_tile_order;
   // cost-ordered work: this launch is ordered by the previous cost map of the same geometry and
   // writes the next one (DESIGN.md §4 "cost-ordered tiles")
-  const bool cost_order = !list && (p->flags & RT_FLAG_COST_ORDER);
+  // (several frames per launch: natural order, and no cost map either -- the same tile position of
+  // every frame finishing together made its atomics contend: +57-86 % on 20-frame launches)
+  const bool cost_order = !list && n_frames == 1 && (p->flags & RT_FLAG_COST_ORDER);
   const bool want_cost = cost_order || (!list && (p->flags & (RT_FLAG_TILE_COST | RT_FLAG_TILE_COST_TIME)));
   int cost_next = -1;
   if (want_cost) {
@@ -2232,7 +2258,12 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
     if (sc->cost_n != n_pos || sc->cost_tiles_x != P.tiles_x) sc->cost_valid = false;   // other geometry
     if (sc->last_ctx >= 0)   // the previous launch (any stream) has finished writing / reading the maps
       HIP_TRY(hipStreamWaitEvent(st, sc->ctx[sc->last_ctx].ev1, 0));
-    if (cost_order && sc->cost_valid) {
+    cost_next = sc->cost_valid ? sc->cost_cur ^ 1 : sc->cost_cur;
+    // ordered: one-frame launches whose head ranges fit one sorting block (multi-frame launches lose
+    // more L2 locality than their drain costs: 20 frames +4.6 % slower ordered, tools/order_probe.py)
+    const bool ordered = cost_order && sc->cost_valid &&
+                         (P.n_tiles + kGroups - 1) / kGroups <= kOrderMaxRange;
+    if (ordered) {
       if (sc->order_cap < P.n_tiles) {
         HIP_TRY(hipDeviceSynchronize());
         if (sc->d_order) HIP_TRY(hipFree(sc->d_order));
@@ -2242,14 +2273,17 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
         sc->order_cap = P.n_tiles;
       }
       hipLaunchKernelGGL(tile_order_kernel, dim3(kGroups), dim3(kOrderThreads), 0, st,
-                         (const uint32_t*)sc->d_cost[sc->cost_cur], sc->d_order, P.n_tiles, n_frames, P.tiles_x);
+                         (const uint32_t*)sc->d_cost[sc->cost_cur], sc->d_order, P.n_tiles, sc->d_cost[cost_next], n_pos);
       HIP_TRY(hipGetLastError());
       P.tile_order = sc->d_order;
+      sc->last_order_n = P.n_tiles;
+    } else {
+      HIP_TRY(hipMemsetAsync(sc->d_cost[cost_next], 0, (size_t)n_pos * sizeof(uint32_t), st));
     }
-    cost_next = sc->cost_valid ? sc->cost_cur ^ 1 : sc->cost_cur;
-    HIP_TRY(hipMemsetAsync(sc->d_cost[cost_next], 0, (size_t)n_pos * sizeof(uint32_t), st));
     P.tile_cost = sc->d_cost[cost_next];
-    P.cost_time = (p->flags & (RT_FLAG_TILE_COST_TIME | RT_FLAG_COST_ORDER)) ? 1 : 0;
+    // cost unit: pixel lifetime (RT_FLAG_TILE_COST_TIME, and RT_FLAG_COST_ORDER alone) or bounces
+    // (RT_FLAG_TILE_COST, also with RT_FLAG_COST_ORDER)
+    P.cost_time = (p->flags & RT_FLAG_TILE_COST) ? 0 : 1;
     sc->cost_n = n_pos;
     sc->cost_tiles_x = P.tiles_x;
   }
@@ -2578,6 +2612,17 @@ long long rt_debug_tile_cost(rt_scene* sc, unsigned int* out, long long n) {
       hipMemcpy(out, sc->d_cost[sc->cost_cur], (size_t)m * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
     return fail(RT_ERR_HIP, "rt_debug_tile_cost: copy failed");
   return sc->cost_n;
+}
+
+long long rt_debug_last_tile_order(rt_scene* sc, unsigned int* out, long long n) {
+  if (!sc) return fail(RT_ERR_INVALID, "rt_debug_last_tile_order: null scene");
+  if (!sc->d_order || sc->last_order_n <= 0) return 0;
+  if (hipSetDevice(sc->device) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+    return fail(RT_ERR_HIP, "rt_debug_last_tile_order: synchronize failed");
+  const long long m = std::min(n, sc->last_order_n);
+  if (out && m > 0 && hipMemcpy(out, sc->d_order, (size_t)m * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
+    return fail(RT_ERR_HIP, "rt_debug_last_tile_order: copy failed");
+  return sc->last_order_n;
 }
 
 int rt_debug_set_tile_order(rt_scene* sc, const unsigned int* order, long long n) {

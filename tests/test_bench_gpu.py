@@ -53,7 +53,9 @@ def test_bench_json_contract_and_saved_frame(tmp_path, frames):
     assert rf["bound"] == "hbm" and rf["peak"] == 8000.0 and rf["kernel_ms_avg"] > 0
     assert rf["frac"] is None or 0.0 < rf["frac"] <= 1.0
     sf = d["single_frame"]
-    assert sf["frames"] == 16 and sf["ms_per_frame"] > 0 and sf["value"] > 0
+    assert sf["frames"] == min(16, frames) and sf["ms_per_frame"] > 0 and sf["value"] > 0
+    co = sf["cost_ordered"]
+    assert co["frames"] == sf["frames"] and co["ms_per_frame"] > 0 and co["rays_per_frame"] == sf["rays_per_frame"]
     ref, rays = expected_frames(320, 180, frames)
     assert np.array_equal(np.load(out), ref)
     assert d["config"]["rays_per_frame"] == rays

@@ -102,10 +102,23 @@ for nf in (1, F):
               f"({(t[0] / base_ms[0] - 1) * 100:+.1f} %), pixels identical: {same}", flush=True)
     lib.rt_debug_set_tile_order(dev._h, None, 0)
     # the library's own cost order (RT_FLAG_COST_ORDER): each launch ordered by the previous one's costs
-    for _ in range(3):
-        launch(nf, abi.RT_FLAG_COST_ORDER)
-    t = timed(nf, REPS, abi.RT_FLAG_COST_ORDER)
-    same = all(torch.equal(a, b) for a, b in zip(ref, bufs[:nf]))
-    print(f"  RT_FLAG_COST_ORDER kernel median {t[0]:.4f} ms mean {t[1]:.4f} "
-          f"({(t[0] / base_ms[0] - 1) * 100:+.1f} %), stream time {t[2]:.4f} ms (unordered {base_ms[2]:.4f}), "
-          f"pixels identical: {same}", flush=True)
+    for fl, nm in ((abi.RT_FLAG_COST_ORDER, "lifetime"), (abi.RT_FLAG_COST_ORDER | abi.RT_FLAG_TILE_COST, "bounces")):
+        for _ in range(3):
+            launch(nf, fl)
+        t = timed(nf, REPS, fl)
+        same = all(torch.equal(a, b) for a, b in zip(ref, bufs[:nf]))
+        if nf == 1:   # the library's order against the host's exact order of the same cost map
+            npos = lib.rt_debug_tile_cost(dev._h, None, 0)
+            cpos = np.zeros(npos, dtype=np.uint32)
+            lib.rt_debug_tile_cost(dev._h, cpos.ctypes.data_as(C.POINTER(C.c_uint)), npos)
+            launch(nf, fl)   # ordered by cpos
+            torch.cuda.synchronize()
+            m = lib.rt_debug_last_tile_order(dev._h, None, 0)
+            got = np.zeros(m, dtype=np.uint32)
+            lib.rt_debug_last_tile_order(dev._h, got.ctypes.data_as(C.POINTER(C.c_uint)), m)
+            want = order_from_costs(cpos, "desc")
+            print(f"   library order == host exact order: {np.array_equal(got, want)} "
+                  f"(first differences at {np.nonzero(got != want)[0][:5]})", flush=True)
+        print(f"  RT_FLAG_COST_ORDER ({nm}) kernel median {t[0]:.4f} ms mean {t[1]:.4f} "
+              f"({(t[0] / base_ms[0] - 1) * 100:+.1f} %), stream time {t[2]:.4f} ms (unordered {base_ms[2]:.4f}), "
+              f"pixels identical: {same}", flush=True)
