@@ -54,3 +54,18 @@ def test_audit_finds_the_round2_hazard_pattern():
                       "\tv_sub_u32_e32 v7, 0, v68"])
     sites = isa_audit.audit(text)
     assert len(sites) == 1 and "s10" in sites[0][2]
+
+
+def test_waitcnt_audit_flags_missing_wait_and_skips_flag_decided_paths():
+    # a use of a loaded register with no s_waitcnt vmcnt on the path is reported ...
+    bad = ["\tglobal_load_dwordx2 v[14:15], v[2:3], off", "\tv_mov_b32_e32 v1, v14", "\ts_endpgm"]
+    assert waitcnt_audit.audit(bad)[1]
+    # ... a use reached only through a branch pair whose flag rules it out is not (both image-store
+    # blocks skipped: s[6:7] = -1 makes "s_andn2_b64 vcc, exec, s[6:7]; s_cbranch_vccnz" fall through)
+    ok = ["\tglobal_load_dwordx2 v[14:15], v[2:3], off", "\ts_mov_b64 s[6:7], -1",
+          "\ts_and_b64 vcc, exec, s[18:19]", "\ts_cbranch_vccz .LBB0_2",
+          "\ts_waitcnt vmcnt(0)", "\tflat_store_dwordx2 v[4:5], v[14:15]", "\ts_mov_b64 s[6:7], 0",
+          ".LBB0_2:", "\ts_andn2_b64 vcc, exec, s[6:7]", "\ts_cbranch_vccnz .LBB0_3",
+          "\ts_waitcnt vmcnt(0)", "\tflat_store_dwordx2 v[4:5], v[14:15]",
+          ".LBB0_3:", "\tv_mov_b32_e32 v1, v14", "\ts_endpgm"]
+    assert waitcnt_audit.audit(ok)[1] == []

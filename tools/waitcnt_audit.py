@@ -17,6 +17,9 @@ LOAD = re.compile(r"^\s*(buffer|global|flat|scratch)_load\w*\s+(v\[(\d+):(\d+)\]
 WAIT = re.compile(r"s_waitcnt\s+(.*)")
 VREG = re.compile(r"v\[(\d+):(\d+)\]|\bv(\d+)\b")
 LABEL = re.compile(r"^(\.LBB[\w_]+):")
+SMOV_CONST = re.compile(r"^\s*s_mov_b64\s+(s\[\d+:\d+\]),\s*(-1|0)\s*$")
+SDEF = re.compile(r"^\s*s_\w+\s+(s\[\d+:\d+\]|s\d+|vcc)\b")
+VCC_FROM = re.compile(r"^\s*s_(and|andn2)_b64\s+vcc,\s*exec,\s*(s\[\d+:\d+\])\s*$")
 BRANCH = re.compile(r"^\s*s_(cbranch_\w+|branch)\s+(\.LBB[\w_]+)")
 
 
@@ -51,12 +54,32 @@ def audit(body, max_depth=6):
     labels = {LABEL.match(l).group(1): i for i, l in enumerate(body) if LABEL.match(l)}
     problems, checked = [], 0
 
-    def walk(i, dst, n_after, depth, seen):
+    # Known SGPR-pair flags along a path: the compiler lowers some if/else chains to a flag set with
+    # s_mov_b64 s[a:b], -1 / 0 and a later "s_andn2_b64 vcc, exec, s[a:b]; s_cbranch_vccnz" -- a
+    # branch whose outcome that flag decides.  Following only the feasible side keeps the audit from
+    # reporting paths the hardware cannot take (e.g. skipping both the fp32 and the fp64 image store).
+    def walk(i, dst, n_after, depth, seen, flags=None, vcc=None):
+        flags = dict(flags or {})
         while i < len(body):
             l = body[i]
-            if (i, n_after) in seen:
+            key = (i, n_after, tuple(sorted(flags.items())), vcc)
+            if key in seen:
                 return
-            seen.add((i, n_after))
+            seen.add(key)
+            mc = SMOV_CONST.match(l)
+            vf = VCC_FROM.match(l)
+            if mc:
+                flags[mc.group(1)] = int(mc.group(2))
+            elif vf:
+                f = flags.get(vf.group(2))
+                # vcc = exec & s (and) or exec & ~s (andn2); exec is non-zero on a live path
+                vcc = None if f is None else ((f != 0) if vf.group(1) == "and" else (f == 0))
+            else:
+                d = SDEF.match(l)
+                if d and not l.lstrip().startswith(("s_cbranch", "s_branch", "s_waitcnt", "s_nop")):
+                    if d.group(1) == "vcc":
+                        vcc = None
+                    flags.pop(d.group(1), None)
             w = WAIT.search(l)
             if w:
                 m = re.search(r"vmcnt\((\d+)\)", w.group(1))
@@ -80,8 +103,17 @@ def audit(body, max_depth=6):
             if VMEM.match(l):
                 n_after += 1
             b = BRANCH.match(l)
+            if b and b.group(1) in ("cbranch_vccnz", "cbranch_vccz") and vcc is not None:
+                taken = vcc if b.group(1) == "cbranch_vccnz" else not vcc
+                if taken:
+                    if b.group(2) not in labels:
+                        return
+                    i = labels[b.group(2)] + 1
+                    continue
+                i += 1
+                continue
             if b and depth < max_depth and b.group(2) in labels:
-                walk(labels[b.group(2)] + 1, dst, n_after, depth + 1, seen)
+                walk(labels[b.group(2)] + 1, dst, n_after, depth + 1, seen, flags, vcc)
                 if b.group(1) == "branch":
                     return
             if op == "s_endpgm":
