@@ -181,7 +181,8 @@ enum : int {
   CD_NODE_ITERS = 16, CD_NODE_LANES, CD_LEAF_ITERS, CD_LEAF_LANES, CD_TRAV_CYCLES, CD_SHADE_CYCLES,
   CD_FETCH_CYCLES, CD_OUTER_ITERS, CD_TRAV_ROUNDS, CD_TRAV_ROUND_LANES, CD_SPILLS, CD_NODE_LINES,
   CD_LEAF_LINES, CD_BIG_LEAF_TESTS, CD_NODE_LDS_ITERS, CD_GUARD = 31,   // CD_GUARD: a wave hit the iteration guard
-  CD_GNODE_UNIFORM = 32, CD_GNODE_DISTINCT, CD_LEAF_UNIFORM
+  CD_GNODE_UNIFORM = 32, CD_GNODE_DISTINCT, CD_LEAF_UNIFORM,
+  CT_ORDER_JOBS = 39   // cost-ordered launches: order / zeroing jobs claimed by blocks that finished
 };
 // Watchdogs (never reached by a correct kernel): the persistent loop, and the wave-level
 // iterations of one traversal round (round, node and leaf loops together).  A wave that
@@ -266,6 +267,12 @@ struct KParams {
   const uint32_t* tile_order;
   uint32_t* tile_cost;
   int cost_time;            // tile_cost in 10-ns ticks of pixel lifetime instead of bounces
+  // cost-ordered launches: blocks whose work is done (the launch's drain, when CUs idle) build the
+  // order of a later launch from a complete cost map and zero the map that launch will fill
+  const uint32_t* order_src;   // complete per-position cost map (an earlier launch's)
+  uint32_t* next_order;        // its tile order, for the launch after this one
+  uint32_t* zero_map;          // cost map to clear for the launch after this one
+  long long n_pos;             // tile positions (= tiles of a one-frame launch)
 };
 
 // ---- fp64 vector ops (course vec4 semantics on xyz) ----
@@ -398,7 +405,8 @@ __device__ __forceinline__ TriOps load_tri(const GTri* tris, uint32_t i) {
 //     fit one batch restarts from the recomputed ambient term).
 // The mirror coefficient comes from the material (the lane keeps the mesh id); the normal of
 // the bounce being shaded lives in the slot's aux words (below).
-enum : int { R_SCOLW = 0, R_PCOL = 1, R_HD = 2, R_LACC = 3, kRegions = 4 };
+//   a suspended traversal (R_SUSP, SUSP variants: cur, postponed leaf, stack pointers, hit so far).
+enum : int { R_SCOLW = 0, R_PCOL = 1, R_HD = 2, R_LACC = 3, R_SUSP = 4, kRegions = 5 };
 #ifndef RT_PS_LANE_REC
 #define RT_PS_LANE_REC 32
 #endif
@@ -444,7 +452,52 @@ __device__ __forceinline__ uint32_t u4c(const uint4& v, int c) {
 // RING: entries of the per-lane traversal-stack ring in LDS (8: room for the 73-node treelet;
 // 16: deep hierarchies, e.g. millions of random triangles, which spill an 8-entry ring often;
 // the treelet then gets what is left, 9 nodes -- rt_scene picks per scene)
-template <int WIDTH, bool STATS, bool TL = false, int RING = kShortStack>
+// ---------------------------------------------------------------------------
+// Cost-ordered work (RT_FLAG_COST_ORDER, one-frame launches): each work head's range of tiles
+// [n h / 8, n (h + 1) / 8) is reordered so its expensive tiles come first, by the cost its tile
+// position had in the previous ordered launch (pixel lifetimes, 10-ns ticks).  A one-frame
+// launch's drain -- waves finishing the paths they started just before the queue ran dry -- is
+// then made of cheap tiles (office 1080p: kernel -11 %, tools/order_probe.py; DESIGN.md §4
+// "cost-ordered tiles").  The order is built inside the render kernel by its first blocks to run
+// out of work, from the cost map of the launch before, so it costs no launch and no busy CU.
+constexpr int kOrderItems = 16;
+constexpr long long kOrderMaxRange = (long long)kBlock * kOrderItems;   // tiles per head range (4096)
+// Sort keys: an 8-bit log-scale cost class (16 per octave, 2^8 .. 2^24 ticks) inverted so that higher
+// costs sort first, above the 12-bit local index; one radix pass over the class bits (stable).
+__device__ __forceinline__ uint32_t order_class(uint32_t cost) {
+  const int q = (int)(__float_as_uint((float)cost) >> 19) - ((127 + 8) << 4);
+  return 255u - (uint32_t)min(255, max(0, q));
+}
+__device__ void order_range(const uint32_t* cost, uint32_t* order, long long n_tiles, int h, unsigned char* lds) {
+  using Sort = rocprim::block_radix_sort<unsigned int, kBlock, kOrderItems>;
+  static_assert(sizeof(typename Sort::storage_type) <= 32768, "sort storage must fit the block's LDS");
+  auto& storage = *reinterpret_cast<typename Sort::storage_type*>(lds);
+  const long long t0 = n_tiles * h / kGroups, t1 = n_tiles * (h + 1) / kGroups;
+  unsigned int keys[kOrderItems];
+#pragma unroll
+  for (int j = 0; j < kOrderItems; ++j) {
+    const long long li = (long long)threadIdx.x * kOrderItems + j;   // local index in the range
+    keys[j] = t0 + li < t1 ? (order_class(cost[t0 + li]) << 12) | (uint32_t)li : 0xffffffffu;   // padding last
+  }
+  Sort().sort(keys, storage, 12, 20);
+#pragma unroll
+  for (int j = 0; j < kOrderItems; ++j) {
+    const long long pos = (long long)threadIdx.x * kOrderItems + j;
+    if (t0 + pos < t1) order[t0 + pos] = (uint32_t)(t0 + (keys[j] & 0xfffu));
+  }
+}
+
+// SUSP: suspend/resume traversal -- once at most kSuspActive lanes of a wave still traverse and work
+// is left, the wave leaves the traversal with those lanes' traversal state parked in path state
+// (R_SUSP; their stacks stay in the LDS ring / spill area), shades its finished lanes, refills its
+// idle ones and resumes the parked rays beside the new ones.  Raises SIMD efficiency where rays of a
+// wave differ widely in length (incoherent scenes); no fan-out in these variants.
+constexpr int kSuspBit = 8;
+#ifndef RT_SUSP_ACTIVE
+#define RT_SUSP_ACTIVE 16
+#endif
+constexpr int kSuspActive = RT_SUSP_ACTIVE;
+template <int WIDTH, bool STATS, bool TL = false, int RING = kShortStack, bool SUSP = false>
 __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render_kernel(KParams P) {
   static_assert(RING >= kMigWords && (RING & (RING - 1)) == 0, "ring: a power of two holding the migration words");
   constexpr int kRingMask = RING - 1;
@@ -735,6 +788,11 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
     }
     // ================= TRAVERSE phase =================
     {
+      bool resumed = false;   // SUSP: this lane's ray resumes a parked traversal
+      if constexpr (SUSP) {
+        resumed = (state & kSuspBit) != 0;
+        state &= ~kSuspBit;
+      }
       const bool anyhit = (state == ST_SHADOW || state == ST_HSHADOW);
       // helpers read their owner's slot (its closest-hit ray and hit distance)
       const int src = (state >= ST_HSHADOW) ? wbase + (int)(htask & 63u) : (int)threadIdx.x;
@@ -834,6 +892,27 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
       float hi_c = round_up_f(tlim - t_off);
       // logical stack [0, sp); the LDS ring holds [slo, sp), spill[] holds [0, slo)
       int sp = 0, slo = 0;
+      bool susp_now = false;   // SUSP: this lane's traversal is parked at the end of this phase
+      uint32_t susp_pleaf = kDone;
+      if constexpr (SUSP) {
+        // the parked record: {cur | postponed leaf << 32, sp | slo << 16 | shadow hit << 31 | best << 32,
+        // best slot, t-limit}; the ray setup above is recomputed bit for bit from the slot
+        if (resumed) {
+          const D2 a = buf_ld2(prs, pvo, (uint32_t)R_SUSP * kRegionBytes);
+          const D2 b = buf_ld2(prs, pvo, (uint32_t)R_SUSP * kRegionBytes + 16u);
+          const unsigned long long w0 = (unsigned long long)__double_as_longlong(a.a);
+          const unsigned long long w1 = (unsigned long long)__double_as_longlong(a.b);
+          cur = (uint32_t)w0;
+          susp_pleaf = (uint32_t)(w0 >> 32);
+          sp = (int)(w1 & 0xffffu);
+          slo = (int)((w1 >> 16) & 0x7fffu);
+          shadow_hit = ((w1 >> 31) & 1ull) != 0ull;
+          best = (int)(uint32_t)(w1 >> 32);
+          best_slot = (int)(uint32_t)__double_as_longlong(b.a);
+          tlim = b.b;
+          hi_c = round_up_f(tlim - t_off);
+        }
+      }
       auto push = [&](uint32_t x) {
         if (sp - slo == RING) {
           spill[(size_t)slo * P.nslots] = stk[(slo & kRingMask) * kBlock];
@@ -937,6 +1016,9 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
           return occluded;
       };
       uint32_t pleaf = kDone;   // 4-wide: postponed leaf
+      if constexpr (SUSP) {
+        if (resumed) pleaf = susp_pleaf;
+      }
 
       uint32_t rounds = 0;
       while (__ballot(cur != kDone || pleaf != kDone) != 0) {
@@ -945,6 +1027,24 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
           cur = kDone;
           pleaf = kDone;
           break;
+        }
+        if constexpr (SUSP) {
+          // few lanes left and work to fetch: park the rest, shade and refill, resume next phase
+          if (heads_left > 0 && __popcll(__ballot(cur != kDone || pleaf != kDone)) <= kSuspActive) {
+            if (cur != kDone || pleaf != kDone) {
+              const unsigned long long w0 = (unsigned long long)cur | ((unsigned long long)pleaf << 32);
+              const unsigned long long w1 = (unsigned long long)((uint32_t)sp | ((uint32_t)slo << 16) |
+                                                                  (shadow_hit ? 0x80000000u : 0u)) |
+                                            ((unsigned long long)(uint32_t)best << 32);
+              buf_st(prs, pvo, (uint32_t)R_SUSP * kRegionBytes, __longlong_as_double((long long)w0));
+              buf_st(prs, pvo, (uint32_t)R_SUSP * kRegionBytes + 8u, __longlong_as_double((long long)w1));
+              buf_st(prs, pvo, (uint32_t)R_SUSP * kRegionBytes + 16u,
+                     __longlong_as_double((long long)(unsigned long long)(uint32_t)best_slot));
+              buf_st(prs, pvo, (uint32_t)R_SUSP * kRegionBytes + 24u, tlim);
+              susp_now = true;
+            }
+            break;
+          }
         }
         if (STATS) wave_tick(d_round_it, d_round_ln, lane);
         if constexpr (TL) wave_tick(tl_wr, tl_dummy, lane);
@@ -1088,6 +1188,9 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
         }
       }
       thit = tlim;
+      if constexpr (SUSP) {
+        if (susp_now) state |= kSuspBit;
+      }
     }
     asm volatile("" ::: "memory");
     if (STATS) { const unsigned long long t = stamp(); d_trav += t - t_stamp; t_stamp = t; }
@@ -1149,7 +1252,9 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
       const int wib = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
       const bool owner = (state == ST_CLOSEST || state == ST_SHADOW);
       const unsigned long long O = __ballot(owner);
-      if (O != 0ull && __popcll(O) <= kDonateMax && *pool_live >= 2u) {
+      // (a wave with parked traversals keeps them: their stacks live in its LDS ring entries)
+      if (O != 0ull && __popcll(O) <= kDonateMax && *pool_live >= 2u &&
+          (!SUSP || __ballot((state & kSuspBit) != 0) == 0ull)) {
         // registers -> this thread's LDS stack entries, then publish the lane mask
         if (owner) {
           // packed: state (3 bits) | shadow hit | frame (< 128) | sample (< 4096) | refl_h + 1 (9 bits);
@@ -1276,7 +1381,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
         refl_h = -1;
         // extra lights of this batch, then the reflection ray once the batch covers every light
         const int rest = P.n_lights - light - 1;
-        want = min(rest, kBatchExtra) + ((rest <= kBatchExtra && mirror_ > 0.0 && depth < P.max_depth) ? 1 : 0);
+        want = SUSP ? 0 : min(rest, kBatchExtra) + ((rest <= kBatchExtra && mirror_ > 0.0 && depth < P.max_depth) ? 1 : 0);
       };
       if (state == ST_SHADOW) {   // batch finished: lights [light, batch_end) in order
         {   // the hit again, from the closest-hit ray and distance kept in the slot
@@ -1576,45 +1681,23 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
       atomicAdd(&P.ctr[CD_BIG_LEAF_TESTS], r);
     }
   }
-}
-
-// ---------------------------------------------------------------------------
-// Cost-ordered work (RT_FLAG_COST_ORDER, one-frame launches): each work head's range of tiles
-// [n h / 8, n (h + 1) / 8) is reordered so its expensive tiles come first, by the cost its tile
-// position had in the previous ordered launch (pixel lifetimes, 10-ns ticks).  A one-frame
-// launch's drain -- waves finishing the paths they started just before the queue ran dry -- is
-// then made of cheap tiles: office 1080p 0.570 -> 0.450 ms with an exact order (tools/
-// order_probe.py; DESIGN.md §4 "cost-ordered tiles").  One block per head range sorts keys
-// (cost descending, then tile index: the order is exact and, among equal costs, spatial) with a
-// block radix sort; the block also zeroes the next cost map.
-constexpr int kOrderThreads = 1024;
-constexpr int kOrderItems = 4;
-constexpr long long kOrderMaxRange = (long long)kOrderThreads * kOrderItems;   // tiles per head range
-__global__ void __launch_bounds__(kOrderThreads) tile_order_kernel(const uint32_t* cost, uint32_t* order, long long n_tiles,
-                                                                   uint32_t* next_cost, long long n_next) {
-  using Sort = rocprim::block_radix_sort<unsigned int, kOrderThreads, kOrderItems>;
-  __shared__ typename Sort::storage_type storage;
-  const long long t0 = n_tiles * blockIdx.x / kGroups, t1 = n_tiles * (blockIdx.x + 1) / kGroups;
-  unsigned int keys[kOrderItems];
-#pragma unroll
-  for (int j = 0; j < kOrderItems; ++j) {
-    const long long li = (long long)threadIdx.x * kOrderItems + j;   // local index in the range
-    keys[j] = 0xffffffffu;                                          // padding sorts last
-    if (t0 + li < t1) {
-      // fp32 bits of the cost: monotonic for costs >= 0; 20 bits (8 exponent + 12 mantissa bits)
-      // inverted so that higher costs sort first, then the 12-bit local index
-      const uint32_t q = __float_as_uint((float)cost[t0 + li]) >> 11;
-      keys[j] = ((0xfffffu - q) << 12) | (uint32_t)li;
+  if (P.zero_map) {
+    // the next launch's work order, built by the first blocks to finish (their CUs would idle in the
+    // drain): job h < 8 sorts head range h of order_src by cost, descending (stable: equal costs keep
+    // the natural band order); jobs 8..15 clear an eighth of zero_map.  The block's LDS is free now.
+    __syncthreads();
+    uint32_t* job = reinterpret_cast<uint32_t*>(lds_raw);
+    if (threadIdx.x == 0) *job = (uint32_t)atomicAdd(&P.ctr[CT_ORDER_JOBS], 1ull);
+    __syncthreads();
+    const uint32_t j = *job;
+    __syncthreads();
+    if (j < (uint32_t)kGroups) {
+      if (P.order_src) order_range(P.order_src, P.next_order, P.n_pos, (int)j, lds_raw);
     }
+    else if (j < 2u * kGroups)
+      for (long long i = P.n_pos * (j - kGroups) / kGroups + threadIdx.x; i < P.n_pos * (j - kGroups + 1) / kGroups; i += kBlock)
+        P.zero_map[i] = 0u;
   }
-  Sort().sort(keys, storage);
-#pragma unroll
-  for (int j = 0; j < kOrderItems; ++j) {
-    const long long pos = (long long)threadIdx.x * kOrderItems + j;
-    if (t0 + pos < t1) order[t0 + pos] = (uint32_t)(t0 + (keys[j] & 0xfffu));
-  }
-  for (long long i = (long long)blockIdx.x * kOrderThreads + threadIdx.x; i < n_next; i += (long long)kGroups * kOrderThreads)
-    next_cost[i] = 0u;
 }
 
 // ---------------------------------------------------------------------------
@@ -1799,10 +1882,15 @@ const Variant kVariants[] = {
     {render_kernel<2, true>, true},
     {render_kernel<4, false, true>, false},
     {render_kernel<4, false, false, 16>, false},
+    {render_kernel<4, false, false, 16, true>, false},
+    {render_kernel<4, false, false, 8, true>, false},
 };
-constexpr int kNumVariants = 5;
+constexpr int kNumVariants = 7;
 constexpr int kRingDeep = 16;
-inline int variant_ring(int v) { return v == 4 ? kRingDeep : kShortStack; }
+inline int variant_ring(int v) { return (v == 4 || v == 5) ? kRingDeep : kShortStack; }
+#ifndef RT_SUSP_MODE
+#define RT_SUSP_MODE 0   // production launches: 0 no suspend/resume, 1 deep scenes, 2 all scenes
+#endif
 // LDS per block: kSlotDoubles doubles of slot, task + visibility words and
 // min(stack_words, ring) stack entries per thread.
 size_t lds_bytes(int stack_words, int ring = kShortStack) {
@@ -1881,15 +1969,18 @@ struct rt_scene {
   GPrim* d_prims = nullptr;     // analytic primitives (rt_scene_set_analytic), spheres then planes
   int n_prims = 0;
   long long table_bytes = 0;    // device bytes of d_mats + d_prims
-  // per-tile-position cost maps (RT_FLAG_COST_ORDER / RT_FLAG_TILE_COST*): the last launch wrote
-  // d_cost[cost_cur] (cost_n positions, tiles_x wide; valid for that geometry)
-  uint32_t* d_cost[2] = {nullptr, nullptr};
+  // per-tile-position cost maps (RT_FLAG_COST_ORDER / RT_FLAG_TILE_COST*) of one image geometry
+  // (cost_n positions, cost_tiles_x wide): launch s of the sequence writes d_cost[s % 3]; an ordered
+  // launch s also builds d_order[(s + 1) % 2] from d_cost[(s - 1) % 3] and clears d_cost[(s + 1) % 3]
+  // in its drain, so launch s + 1 is ordered by the costs of launch s - 1
+  uint32_t* d_cost[3] = {nullptr, nullptr, nullptr};
+  uint32_t* d_order[2] = {nullptr, nullptr};
   long long cost_cap = 0, cost_n = 0;
-  int cost_tiles_x = 0, cost_cur = 0;
-  bool cost_valid = false;
-  uint32_t* d_order = nullptr;        // RT_FLAG_COST_ORDER: this launch's tile order
-  long long order_cap = 0;
+  int cost_tiles_x = 0;
+  long long cost_seq = 0;             // launches of the current sequence
+  long long order_for = -1;           // the sequence launch d_order[order_for % 2] was built for
   long long last_order_n = 0;         // tiles of the last ordered launch (rt_debug_last_tile_order)
+  int last_order_buf = 0;
   uint32_t* d_tile_order = nullptr;  // rt_debug_set_tile_order: work order of launches with that many tiles
   long long tile_order_n = 0;
 };
@@ -2234,64 +2325,66 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   P.list_count = count;
   P.sample_out = sample_out;
   if (!list && sc->d_tile_order && sc->tile_order_n == P.n_tiles) P.tile_order = sc->d_tile_order;
-  // cost-ordered work: this launch is ordered by the previous cost map of the same geometry and
-  // writes the next one (DESIGN.md §4 "cost-ordered tiles")
-  // (several frames per launch: natural order, and no cost map either -- the same tile position of
-  // every frame finishing together made its atomics contend: +57-86 % on 20-frame launches)
+  // cost-ordered work (one-frame launches): ordered by the costs of the launch before the previous
+  // one of the same geometry, while this launch's costs are recorded
+  // (several frames per launch: natural order and no cost map -- the same tile position of every
+  // frame finishing together made the cost atomics contend: +57-86 % on 20-frame launches)
   const bool cost_order = !list && n_frames == 1 && (p->flags & RT_FLAG_COST_ORDER);
-  const bool want_cost = cost_order || (!list && (p->flags & (RT_FLAG_TILE_COST | RT_FLAG_TILE_COST_TIME)));
-  int cost_next = -1;
-  if (want_cost) {
+  const bool cost_debug = !list && (p->flags & (RT_FLAG_TILE_COST | RT_FLAG_TILE_COST_TIME));
+  if (cost_order || cost_debug) {
     const long long n_pos = (long long)P.tiles_x * ((rows + 7) / 8);
     if (sc->cost_cap < n_pos) {
-      HIP_TRY(hipDeviceSynchronize());   // launches in flight may still use the old maps
-      for (int k = 0; k < 2; ++k) {
-        if (sc->d_cost[k]) HIP_TRY(hipFree(sc->d_cost[k]));
-        sc->d_cost[k] = nullptr;
-      }
+      HIP_TRY(hipDeviceSynchronize());   // launches in flight may still use the old buffers
+      for (uint32_t*& q : sc->d_cost) { if (q) HIP_TRY(hipFree(q)); q = nullptr; }
+      for (uint32_t*& q : sc->d_order) { if (q) HIP_TRY(hipFree(q)); q = nullptr; }
       sc->cost_cap = 0;
-      sc->cost_valid = false;
-      for (int k = 0; k < 2; ++k)
-        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&sc->d_cost[k]), (size_t)n_pos * sizeof(uint32_t)));
+      for (uint32_t*& q : sc->d_cost) HIP_TRY(hipMalloc(reinterpret_cast<void**>(&q), (size_t)n_pos * sizeof(uint32_t)));
+      for (uint32_t*& q : sc->d_order) HIP_TRY(hipMalloc(reinterpret_cast<void**>(&q), (size_t)n_pos * sizeof(uint32_t)));
       sc->cost_cap = n_pos;
+      sc->cost_seq = 0;
     }
-    if (sc->cost_n != n_pos || sc->cost_tiles_x != P.tiles_x) sc->cost_valid = false;   // other geometry
-    if (sc->last_ctx >= 0)   // the previous launch (any stream) has finished writing / reading the maps
+    if (sc->cost_n != n_pos || sc->cost_tiles_x != P.tiles_x) sc->cost_seq = 0;   // another geometry
+    sc->cost_n = n_pos;
+    sc->cost_tiles_x = P.tiles_x;
+    if (sc->last_ctx >= 0)   // the previous launch (any stream) has finished with the maps
       HIP_TRY(hipStreamWaitEvent(st, sc->ctx[sc->last_ctx].ev1, 0));
-    cost_next = sc->cost_valid ? sc->cost_cur ^ 1 : sc->cost_cur;
-    // ordered: one-frame launches whose head ranges fit one sorting block (multi-frame launches lose
-    // more L2 locality than their drain costs: 20 frames +4.6 % slower ordered, tools/order_probe.py)
-    const bool ordered = cost_order && sc->cost_valid &&
-                         (P.n_tiles + kGroups - 1) / kGroups <= kOrderMaxRange;
-    if (ordered) {
-      if (sc->order_cap < P.n_tiles) {
-        HIP_TRY(hipDeviceSynchronize());
-        if (sc->d_order) HIP_TRY(hipFree(sc->d_order));
-        sc->d_order = nullptr;
-        sc->order_cap = 0;
-        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&sc->d_order), (size_t)P.n_tiles * sizeof(uint32_t)));
-        sc->order_cap = P.n_tiles;
-      }
-      hipLaunchKernelGGL(tile_order_kernel, dim3(kGroups), dim3(kOrderThreads), 0, st,
-                         (const uint32_t*)sc->d_cost[sc->cost_cur], sc->d_order, P.n_tiles, sc->d_cost[cost_next], n_pos);
-      HIP_TRY(hipGetLastError());
-      P.tile_order = sc->d_order;
-      sc->last_order_n = P.n_tiles;
-    } else {
-      HIP_TRY(hipMemsetAsync(sc->d_cost[cost_next], 0, (size_t)n_pos * sizeof(uint32_t), st));
-    }
-    P.tile_cost = sc->d_cost[cost_next];
     // cost unit: pixel lifetime (RT_FLAG_TILE_COST_TIME, and RT_FLAG_COST_ORDER alone) or bounces
     // (RT_FLAG_TILE_COST, also with RT_FLAG_COST_ORDER)
     P.cost_time = (p->flags & RT_FLAG_TILE_COST) ? 0 : 1;
-    sc->cost_n = n_pos;
-    sc->cost_tiles_x = P.tiles_x;
+    if (!cost_order) {   // diagnostics: a fresh map, the first launch of a new sequence
+      sc->cost_seq = 0;
+      HIP_TRY(hipMemsetAsync(sc->d_cost[0], 0, (size_t)n_pos * sizeof(uint32_t), st));
+      P.tile_cost = sc->d_cost[0];
+      sc->cost_seq = 1;
+      sc->order_for = -1;
+    } else {
+      const long long q = sc->cost_seq;
+      if (q == 0)
+        for (uint32_t* m : sc->d_cost) HIP_TRY(hipMemsetAsync(m, 0, (size_t)n_pos * sizeof(uint32_t), st));
+      P.tile_cost = sc->d_cost[q % 3];
+      if (sc->order_for == q) {
+        P.tile_order = sc->d_order[q % 2];
+        sc->last_order_n = P.n_tiles;
+        sc->last_order_buf = (int)(q % 2);
+      }
+      if ((n_pos + kGroups - 1) / kGroups <= kOrderMaxRange) {   // the drain jobs: next order, next map cleared
+        P.order_src = q >= 1 ? sc->d_cost[(q + 2) % 3] : nullptr;
+        P.next_order = sc->d_order[(q + 1) % 2];
+        P.zero_map = sc->d_cost[(q + 1) % 3];
+        P.n_pos = n_pos;
+        if (q >= 1) sc->order_for = q + 1;
+      } else {
+        HIP_TRY(hipMemsetAsync(sc->d_cost[(q + 1) % 3], 0, (size_t)n_pos * sizeof(uint32_t), st));
+      }
+      sc->cost_seq = q + 1;
+    }
   }
 
   const int v = (p->flags & RT_FLAG_TRAVERSAL_STATS) ? 2
                 : (p->flags & RT_FLAG_WIDE_STATS) ? 1
                 : (p->flags & RT_FLAG_TIMELINE) ? 3
-                : sc->deep ? 4 : 0;   // 4: the 16-entry-ring production variant
+                : sc->deep ? (RT_SUSP_MODE >= 1 ? 5 : 4)   // 4/5: the 16-entry-ring production variants
+                : (RT_SUSP_MODE >= 2 ? 6 : 0);
   const int ring = variant_ring(v);
   const int n_top = sc->n_top_v[v];
   const size_t lds = lds_bytes_total(sc->stack_words, n_top, ring);
@@ -2340,10 +2433,6 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
                             args, lds, st));
   }
   HIP_TRY(hipEventRecord(C.ev1, st));
-  if (cost_next >= 0) {   // this launch's costs order the next ordered launch of this geometry
-    sc->cost_cur = cost_next;
-    sc->cost_valid = true;
-  }
   C.used = true;
   C.variant = v;
   C.waves = rows > 0 ? blocks * (kBlock / 64) : 0;
@@ -2604,23 +2693,24 @@ int rt_debug_blocks_per_cu(rt_scene* sc, int variant) {
 
 long long rt_debug_tile_cost(rt_scene* sc, unsigned int* out, long long n) {
   if (!sc) return fail(RT_ERR_INVALID, "rt_debug_tile_cost: null scene");
-  if (!sc->cost_valid) return 0;
+  if (sc->cost_seq < 1) return 0;
   if (hipSetDevice(sc->device) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
     return fail(RT_ERR_HIP, "rt_debug_tile_cost: synchronize failed");
   const long long m = std::min(n, sc->cost_n);
   if (out && m > 0 &&
-      hipMemcpy(out, sc->d_cost[sc->cost_cur], (size_t)m * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
+      hipMemcpy(out, sc->d_cost[(sc->cost_seq - 1) % 3], (size_t)m * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
     return fail(RT_ERR_HIP, "rt_debug_tile_cost: copy failed");
   return sc->cost_n;
 }
 
 long long rt_debug_last_tile_order(rt_scene* sc, unsigned int* out, long long n) {
   if (!sc) return fail(RT_ERR_INVALID, "rt_debug_last_tile_order: null scene");
-  if (!sc->d_order || sc->last_order_n <= 0) return 0;
+  if (!sc->d_order[0] || sc->last_order_n <= 0) return 0;
   if (hipSetDevice(sc->device) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
     return fail(RT_ERR_HIP, "rt_debug_last_tile_order: synchronize failed");
   const long long m = std::min(n, sc->last_order_n);
-  if (out && m > 0 && hipMemcpy(out, sc->d_order, (size_t)m * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
+  if (out && m > 0 &&
+      hipMemcpy(out, sc->d_order[sc->last_order_buf], (size_t)m * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
     return fail(RT_ERR_HIP, "rt_debug_last_tile_order: copy failed");
   return sc->last_order_n;
 }
@@ -2741,7 +2831,7 @@ void rt_scene_free(rt_scene* sc) {
   if (!sc) return;
   (void)hipSetDevice(sc->device);
   (void)hipDeviceSynchronize();   // launches may still be reading the scene
-  void* ptrs[] = {sc->d_cost[0], sc->d_cost[1], sc->d_order, sc->d_tile_order, sc->d_nodes, sc->d_nodes4, sc->d_tris, sc->d_shade, sc->d_tnorm, sc->d_tu,
+  void* ptrs[] = {sc->d_cost[0], sc->d_cost[1], sc->d_cost[2], sc->d_order[0], sc->d_order[1], sc->d_tile_order, sc->d_nodes, sc->d_nodes4, sc->d_tris, sc->d_shade, sc->d_tnorm, sc->d_tu,
                   sc->d_tv, sc->d_texels, sc->d_mats, sc->d_lights, sc->d_slot2dev, sc->d_prims};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);

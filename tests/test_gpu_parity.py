@@ -227,7 +227,8 @@ def test_tile_order_and_costs_change_no_pixel(nf):
     ref, rc = render()
     n_tiles = 25 * 15 * nf
     for flag in (rtamd.abi.RT_FLAG_TILE_COST, rtamd.abi.RT_FLAG_TILE_COST_TIME, rtamd.abi.RT_FLAG_COST_ORDER,
-                 rtamd.abi.RT_FLAG_COST_ORDER):   # (the second ordered launch follows the first one's costs)
+                 rtamd.abi.RT_FLAG_COST_ORDER, rtamd.abi.RT_FLAG_COST_ORDER,
+                 rtamd.abi.RT_FLAG_COST_ORDER):   # (one-frame: ordered from the third on, by the costs of two before)
         img, c = render(flag)
         assert all(np.array_equal(a, b) for a, b in zip(img, ref)) and c == rc
         n = lib.rt_debug_tile_cost(dev._h, None, 0)
@@ -235,6 +236,12 @@ def test_tile_order_and_costs_change_no_pixel(nf):
         cost = np.zeros(n, dtype=np.uint32)
         lib.rt_debug_tile_cost(dev._h, cost.ctypes.data_as(C.POINTER(C.c_uint)), n)
         assert cost.min() > 0
+    if nf == 1:   # the ordered launches used a permutation of the tiles
+        m = lib.rt_debug_last_tile_order(dev._h, None, 0)
+        assert m == n_tiles
+        got = np.zeros(m, dtype=np.uint32)
+        lib.rt_debug_last_tile_order(dev._h, got.ctypes.data_as(C.POINTER(C.c_uint)), m)
+        assert np.array_equal(np.sort(got), np.arange(n_tiles))
     order = np.random.default_rng(5).permutation(n_tiles).astype(np.uint32)
     assert lib.rt_debug_set_tile_order(dev._h, order.ctypes.data_as(C.POINTER(C.c_uint)), n_tiles) == 0
     img, c = render()
