@@ -496,7 +496,7 @@ constexpr int kSuspBit = 8;
 #ifndef RT_SUSP_ACTIVE
 #define RT_SUSP_ACTIVE 16
 #endif
-constexpr int kSuspActive = RT_SUSP_ACTIVE;
+constexpr int kSuspActive = RT_SUSP_ACTIVE;   // 16 (config 4: 8 +2.8 %, 16 +3.2 %, 32 +1.8 %, 48 -8 %)
 template <int WIDTH, bool STATS, bool TL = false, int RING = kShortStack, bool SUSP = false>
 __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render_kernel(KParams P) {
   static_assert(RING >= kMigWords && (RING & (RING - 1)) == 0, "ring: a power of two holding the migration words");
@@ -1889,7 +1889,7 @@ constexpr int kNumVariants = 7;
 constexpr int kRingDeep = 16;
 inline int variant_ring(int v) { return (v == 4 || v == 5) ? kRingDeep : kShortStack; }
 #ifndef RT_SUSP_MODE
-#define RT_SUSP_MODE 0   // production launches: 0 no suspend/resume, 1 deep scenes, 2 all scenes
+#define RT_SUSP_MODE 1   // suspend/resume: 0 never, 1 several-frame launches of deep scenes, 2 all launches (A/B)
 #endif
 // LDS per block: kSlotDoubles doubles of slot, task + visibility words and
 // min(stack_words, ring) stack entries per thread.
@@ -2383,7 +2383,9 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   const int v = (p->flags & RT_FLAG_TRAVERSAL_STATS) ? 2
                 : (p->flags & RT_FLAG_WIDE_STATS) ? 1
                 : (p->flags & RT_FLAG_TIMELINE) ? 3
-                : sc->deep ? (RT_SUSP_MODE >= 1 ? 5 : 4)   // 4/5: the 16-entry-ring production variants
+                // 4/5: the 16-entry-ring production variants; suspend/resume on deep scenes' several-
+                // frame launches (config 4, 128 frames: +3.2 %; one frame: -6 %, so not there)
+                : sc->deep ? ((RT_SUSP_MODE >= 2 || (RT_SUSP_MODE == 1 && n_frames > 1 && !list)) ? 5 : 4)
                 : (RT_SUSP_MODE >= 2 ? 6 : 0);
   const int ring = variant_ring(v);
   const int n_top = sc->n_top_v[v];

@@ -735,6 +735,28 @@ def test_stack_ring_depth_changes_no_pixel(kind, kw, w, h, spp):
     assert counts(sb) == [cnt.primary_rays, cnt.shadow_rays, cnt.reflection_rays]
 
 
+@pytest.mark.parametrize("kw,w,h", [({"n_triangles": 200000}, 160, 90), ({"n_triangles": 300000}, 192, 108)])
+def test_suspend_resume_frames_equal_single_launches(kw, w, h):
+    # Deep scenes' several-frame launches run the suspend/resume variant (waves park their last
+    # few rays, shade and refill, then resume them): every frame equals its own one-frame launch
+    # (the plain deep variant) bit for bit, with the same ray counts, and the oracle.
+    import torch
+    hs, dev, orc = Case.get("random_tris", **kw)
+    base = hs.render_params(w, h, 1)
+    base.out_format = rtamd.RT_OUT_RGB_F64
+    cams = [rtamd.camera_orbit(base, 0.05 * f) for f in range(4)]
+    outs = [torch.full((h, w, 3), float("nan"), dtype=torch.float64, device="cuda") for _ in cams]
+    st = dev.launch_frames(cams, [o.data_ptr() for o in outs], stats=True)
+    rays = 0
+    for f, cam in enumerate(cams):
+        ref, rst = dev.render(cam)
+        assert np.array_equal(outs[f].cpu().numpy(), ref), f
+        rays += sum(counts(rst))
+    assert sum(counts(st)) == rays
+    ref0, cnt = orc.render(cams[0], pyoracle.MODE_ORDERED, threads=0)
+    assert np.abs(outs[0].cpu().numpy() - ref0).max() <= TOL64
+
+
 def test_unknown_device_tree_fails_loudly():
     hs, _, _ = Case.get("cornell")
     with pytest.raises(ValueError):
