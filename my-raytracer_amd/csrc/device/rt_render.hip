@@ -193,6 +193,31 @@ constexpr unsigned kTravGuard = 1u << 24;
 constexpr int kTlCap = 256;   // TL variant: traversal rounds recorded per wave
 constexpr int kTlWords = 8;   // ... and words per round
 
+// Division of 32-bit n < 2^31 by a launch-invariant d >= 1 as mulhi(n, m) >> s (Granlund-Montgomery;
+// m, s chosen on the host so that the quotient is exact for every n < 2^31): 2 VALU instead of
+// the ~20 of a 32-bit (or the SALU/VALU mix of a 64-bit) division in the refill's tile decode.
+struct DivMagic {
+  uint32_t m, s;
+  __host__ __device__ uint32_t div(uint32_t n) const {   // m == 0: d == 1 (m would need 33 bits)
+#ifdef __HIP_DEVICE_COMPILE__
+    return m ? __umulhi(n, m) >> s : n;
+#else
+    return m ? (uint32_t)(((unsigned long long)n * m) >> 32) >> s : n;
+#endif
+  }
+};
+inline DivMagic div_magic(uint32_t d) {
+  // smallest s with m = ceil(2^(32+s) / d) < 2^32 and error e = m d - 2^(32+s) < 2^(s+1), which makes
+  // floor(n m / 2^(32+s)) = floor(n / d) for all n < 2^31 (e n < 2^(32+s))
+  for (uint32_t s = 0; s < 32; ++s) {
+    const unsigned __int128 p = (unsigned __int128)1 << (32 + s);
+    const unsigned __int128 m = (p + d - 1) / d;
+    if (m >> 32) continue;
+    const unsigned __int128 e = m * d - p;
+    if ((e << 31) < p) return DivMagic{(uint32_t)m, s};
+  }
+  return DivMagic{0u, 0u};   // unreachable for d >= 1
+}
 constexpr int kMaxFrames = RT_MAX_FRAMES;   // frames per launch
 // adaptive-pass list entries: frame << 25 | local pixel id (lrow * W + x)
 constexpr int kListFrameShift = 25;
@@ -267,6 +292,7 @@ struct KParams {
   const uint32_t* tile_order;
   uint32_t* tile_cost;
   int cost_time;            // tile_cost in 10-ns ticks of pixel lifetime instead of bounces
+  DivMagic div_row_tiles, div_tiles_x, div_stripe_h;   // n / (frames x tiles_x), n / tiles_x, n / stripe_h
   // cost-ordered launches: blocks whose work is done (the launch's drain, when CUs idle) build the
   // order of a later launch from a complete cost map and zero the map that launch will fill
   const uint32_t* order_src;   // complete per-position cost map (an earlier launch's)
@@ -371,6 +397,13 @@ __device__ __forceinline__ void wave_distinct(uint32_t key, unsigned long long& 
     n++;
   }
   if (lane == first) acc += n;
+}
+
+// global row of local (packed) row lrow of a striped shard: (lrow / h) * count + index stripes of h rows
+__device__ __forceinline__ int stripe_row(const KParams& P, int lrow) {
+  const uint32_t st = P.div_stripe_h.div((uint32_t)lrow);
+  return (int)((st * (uint32_t)P.stripe_count + (uint32_t)P.stripe_index) * (uint32_t)P.stripe_h +
+               ((uint32_t)lrow - st * (uint32_t)P.stripe_h));
 }
 
 struct TriOps {
@@ -716,15 +749,17 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
             item = wk;
           } else {
 #if RT_BAND_ORDER
-            const long long tile = P.tile_order ? (long long)P.tile_order[wk >> 6] : (wk >> 6);
+            // (tile indices < 2^31, checked at launch: 32-bit divisions by the launch's invariant
+            // divisors as a multiply-high and a shift, DivMagic)
+            const uint32_t tile = P.tile_order ? P.tile_order[wk >> 6] : (uint32_t)(wk >> 6);
             const int j = (int)(wk & 63);
             // several frames: tile row ty of every frame, then row ty + 1, so each XCD head's
             // contiguous range is a band of rows of all frames (its L2 holds one band's nodes)
-            const long long row_tiles = (long long)P.n_frames * P.tiles_x;
-            const long long ty = tile / row_tiles;
-            const long long rem = tile - ty * row_tiles;
-            frame = P.n_frames > 1 ? (int)(rem / P.tiles_x) : 0;
-            const int tx = (int)(rem - (long long)frame * P.tiles_x);
+            const uint32_t row_tiles = (uint32_t)P.n_frames * (uint32_t)P.tiles_x;
+            const uint32_t ty = P.div_row_tiles.div(tile);
+            const uint32_t rem = tile - ty * row_tiles;
+            frame = P.n_frames > 1 ? (int)P.div_tiles_x.div(rem) : 0;
+            const int tx = (int)(rem - (uint32_t)frame * (uint32_t)P.tiles_x);
 #else
             long long tile = wk >> 6;
             const int j = (int)(wk & 63);
@@ -739,7 +774,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
           if (px < P.W && lrow < P.rows) {
             py = (P.stripe_count == 1)
                      ? P.row_begin + lrow
-                     : ((lrow / P.stripe_h) * P.stripe_count + P.stripe_index) * P.stripe_h + (lrow % P.stripe_h);
+                     : stripe_row(P, lrow);
             sample = P.list ? (int)(item % P.nsamp) : 0;
             start_sample();
           }
@@ -1334,7 +1369,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
             lrow = (int)(v_[7] >> 16);
             py = (P.stripe_count == 1)
                      ? P.row_begin + lrow
-                     : ((lrow / P.stripe_h) * P.stripe_count + P.stripe_index) * P.stripe_h + (lrow % P.stripe_h);
+                     : stripe_row(P, lrow);
             lvis[threadIdx.x] = lvis[t];
 #pragma unroll
             for (int k = 0; k < kSlotDoubles; ++k) lds_d[k * kBlock + threadIdx.x] = lds_d[k * kBlock + t];
@@ -2321,6 +2356,10 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   P.nsamp = p->spp_n * p->spp_n;
   P.frame_tiles = list ? (list_cap * P.nsamp + 63) / 64 : (long long)P.tiles_x * ((rows + 7) / 8);
   P.n_tiles = P.frame_tiles * n_frames;
+  if (P.n_tiles >= (1LL << 31)) return fail(RT_ERR_INVALID, "rt_launch: more than 2^31 tiles in one launch");
+  P.div_row_tiles = div_magic((uint32_t)P.tiles_x * (uint32_t)n_frames);
+  P.div_tiles_x = div_magic((uint32_t)P.tiles_x);
+  P.div_stripe_h = div_magic((uint32_t)P.stripe_h);
   P.list = list;
   P.list_count = count;
   P.sample_out = sample_out;
