@@ -412,7 +412,7 @@ def main():
                 "host_bvh_build_s": round(build_s, 4),
                 # frames the production kernel rendered in this process (counting launches, warm-up,
                 # timed run, single-frame run): the divisor tools/pmc_summary.py uses for per-frame bytes
-                "production_frames_rendered": (F + rem + 1 + a.warmup + a.steps + (3 * NS if single else 0)
+                "production_frames_rendered": (F + rem + NS + a.warmup + a.steps + (3 * NS if single else 0)
                                                if not a.adaptive else None),
                 "device_scene_MB": round(gpu.device_bytes / 1e6, 1),
                 **({"upload_options": upload_opts} if upload_opts else {}),

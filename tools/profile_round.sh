@@ -35,5 +35,8 @@ if [ ! -f $CAL ]; then
   timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/calib_write -o run -- ./tools/hbm_calib.bin > $O/calib_write.log 2>&1
   python tools/calib_summary.py $CAL $O/calib_fetch $O/calib_write > /dev/null
 fi
-python tools/pmc_summary.py $O/pmc_$TAG.json --bench $O/bench_$TAG.json --calib $CAL $O/pmc_${TAG}_*/
+# (the passes of this tag only: a glob pmc_${TAG}_*/ would also take those of a tag that extends it)
+python tools/pmc_summary.py $O/pmc_$TAG.json --bench $O/bench_$TAG.json --calib $CAL \
+  $O/pmc_${TAG}_fetch $O/pmc_${TAG}_write $O/pmc_${TAG}_td $O/pmc_${TAG}_ta $O/pmc_${TAG}_tcc $O/pmc_${TAG}_tcp \
+  $O/pmc_${TAG}_sq $O/pmc_${TAG}_sqa $O/pmc_${TAG}_valu
 echo "profile $TAG done"
