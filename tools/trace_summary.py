@@ -4,10 +4,12 @@ bench.py (dev tool).
 usage: python tools/trace_summary.py OUT.json PROF_DIR BENCH.json
 
 bench.py's production-kernel dispatches come in a fixed order: the counting launch of F frames
-(plus one of steps % F frames when F does not divide --steps), the frame-0 counting launch, the
-warm-up launches, the timed launches, then --single-frames one-frame launches.  The summary
-averages the timed launches and the single-frame launches separately, so each figure can be set
-beside the bench's own HIP-event kernel_ms_avg / single_frame.kernel_ms_avg.
+(plus one of steps % F frames when F does not divide --steps), the counting launch of the NS
+single-frame views, the warm-up launches, the timed launches, then three runs of NS one-frame
+launches: the single-frame record, an untimed RT_FLAG_COST_ORDER pass, and the cost-ordered
+record.  The summary averages the timed launches and each single-frame record separately, so each
+figure can be set beside the bench's own HIP-event kernel_ms_avg / single_frame.kernel_ms_avg /
+single_frame.cost_ordered.kernel_ms_avg.
 """
 import csv
 import glob
@@ -36,17 +38,23 @@ def main():
     n_count = 1 + (1 if steps % F else 0) + 1
     n_warm = -(-warm // F) if warm else 0
     n_single = bench["single_frame"]["frames"] if bench.get("single_frame") else 0
-    timed = dur[n_count + n_warm:n_count + n_warm + n_timed]
-    single = dur[n_count + n_warm + n_timed:n_count + n_warm + n_timed + n_single]
+    t0 = n_count + n_warm
+    timed = dur[t0:t0 + n_timed]
+    single = dur[t0 + n_timed:t0 + n_timed + n_single]
+    ordered = dur[t0 + n_timed + 2 * n_single:t0 + n_timed + 3 * n_single]
+    sf = bench.get("single_frame") or {}
     res = {
         "production_dispatches": len(dur),
-        "expected_dispatches": n_count + n_warm + n_timed + n_single,
+        "expected_dispatches": n_count + n_warm + n_timed + 3 * n_single,
         "timed_launches": len(timed),
         "timed_ms_avg": sum(timed) / len(timed) if timed else None,
         "bench_kernel_ms_avg": bench["roofline"]["kernel_ms_avg"],
         "single_frame_launches": len(single),
         "single_ms_avg": sum(single) / len(single) if single else None,
-        "bench_single_kernel_ms_avg": bench["single_frame"]["kernel_ms_avg"] if bench.get("single_frame") else None,
+        "bench_single_kernel_ms_avg": sf.get("kernel_ms_avg"),
+        "cost_ordered_launches": len(ordered),
+        "cost_ordered_ms_avg": sum(ordered) / len(ordered) if ordered else None,
+        "bench_cost_ordered_kernel_ms_avg": (sf.get("cost_ordered") or {}).get("kernel_ms_avg"),
         "all_ms": [round(d, 4) for d in dur],
         "source": os.path.normpath(pdir),
     }
