@@ -373,7 +373,7 @@ def main():
                         "td_busy_frac": pmc.get("td_busy_frac") if pmc else None,
                         "def": "128*wide_node_visits + 80*tri_tests + 96*closest_hits (production kernel) / "
                                "(64 B/clk x 256 CUs x 2.4 GHz)"},
-            "wave_cycles": pmc_wave_mix(workload_key(a, n)),
+            "wave_cycles": pmc_wave_mix(workload_key(a, n), frames_per_launch),
         })
         out = {
             "metric": "Mrays/sec (primary+shadow+reflect), Office 1920x1080 1spp",
@@ -486,19 +486,27 @@ def pmc_per_frame(key, frames_per_launch=None):
             "td_busy_frac": d.get("_derived", {}).get("td_busy_frac"), "source": str(path.relative_to(ROOT))}
 
 
-def pmc_wave_mix(key):
-    """Where a wave's cycles go (rocprofv3 SQ counters of this workload, newest committed summary):
+def pmc_wave_mix(key, frames_per_launch=None):
+    """Where a wave's cycles go (rocprofv3 SQ counters of this workload, newest committed summary;
+    within that round the one profiled at the same frames per launch, as pmc_per_frame picks):
     issuing an instruction, waiting on a memory counter, the rest (ready behind the SIMD's other
     waves); None when no such pass was committed."""
+    cands = []
     for path, d in _newest_first(key):
         try:
             wc = d["SQ_WAVE_CYCLES"]["sum"]
             issue, wait = d["SQ_ACTIVE_INST_ANY"]["sum"] / wc, d["SQ_WAIT_ANY"]["sum"] / wc
         except (KeyError, TypeError, ZeroDivisionError):
             continue
-        return {"issue_frac": round(issue, 3), "mem_wait_frac": round(wait, 3),
-                "other_frac": round(1.0 - issue - wait, 3), "source": str(path.relative_to(ROOT))}
-    return None
+        cands.append((_profile_tag(path), path, d, issue, wait))
+    if not cands:
+        return None
+    same_round = [c for c in cands if c[0] == cands[0][0]]
+    _, path, d, issue, wait = next((c for c in same_round if frames_per_launch is not None
+                                    and c[2].get("_bench", {}).get("frames_per_launch") == frames_per_launch),
+                                   same_round[0])
+    return {"issue_frac": round(issue, 3), "mem_wait_frac": round(wait, 3),
+            "other_frac": round(1.0 - issue - wait, 3), "source": str(path.relative_to(ROOT))}
 
 
 def usable_cpus():
