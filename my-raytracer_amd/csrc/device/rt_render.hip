@@ -535,7 +535,11 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
   static_assert(RING >= kMigWords && (RING & (RING - 1)) == 0, "ring: a power of two holding the migration words");
   constexpr int kRingMask = RING - 1;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
-  double* lds_d = reinterpret_cast<double*>(lds_raw);
+  // LDS: [stack ring: RING rows of kBlock words][slots: kSlotDoubles x kBlock doubles][task words]
+  // [visibility words][treelet][lights][pool] -- the ring at address 0 (below)
+  constexpr uint32_t kRingRegion = (uint32_t)RING * kBlock * sizeof(uint32_t);
+  unsigned char* const lds_s = lds_raw + kRingRegion;
+  double* lds_d = reinterpret_cast<double*>(lds_s);
   RaySlots R;
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
@@ -545,9 +549,13 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
   R.tlim = lds_d + 6 * kBlock + threadIdx.x;
 #pragma unroll
   for (int k = 0; k < 3; ++k) R.a[k] = lds_d + (7 + k) * kBlock + threadIdx.x;
-  uint32_t* ltask = reinterpret_cast<uint32_t*>(lds_raw + kSlotDoubles * kBlock * sizeof(double));   // [kBlock]
+  uint32_t* ltask = reinterpret_cast<uint32_t*>(lds_s + kSlotDoubles * kBlock * sizeof(double));   // [kBlock]
   uint32_t* lvis = ltask + kBlock;                                                             // [kBlock]
-  uint32_t* stk = lvis + kBlock + threadIdx.x;
+  uint32_t* stk = reinterpret_cast<uint32_t*>(lds_raw) + threadIdx.x;
+  // the ring as plain LDS byte addresses: the render kernels have no static LDS, so the dynamic
+  // block, and the ring with it, starts at LDS address 0; this lane's byte offset within a ring row
+  // sits below the row stride, so a ring address is one AND-OR (push / pop below)
+  const uint32_t lane_b = threadIdx.x * 4u;
   lvis[threadIdx.x] = 0u;
   // compaction pool: [0] waves of the block still running and not donors, [1..] per wave the
   // lanes it handed over (bits cleared as other waves adopt them)
@@ -925,8 +933,12 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
       const float oix = ofx * ivx, oiy = ofy * ivy, oiz = ofz * ivz;
       const float lo_c = round_down_f(-t_off);
       float hi_c = round_up_f(tlim - t_off);
-      // logical stack [0, sp); the LDS ring holds [slo, sp), spill[] holds [0, slo)
-      int sp = 0, slo = 0;
+      // logical stack [0, sp); the LDS ring holds [slo, sp), spill[] holds [0, slo).  Kept byte-scaled
+      // by a lane's ring stride (kSW = kBlock words, in bytes): sq = sp * kSW, sqlim = (slo + RING) * kSW, so a
+      // push is one compare with sqlim, one AND-OR for the ring address (the lane's byte offset sits
+      // below kSW) and one add; sp / slo themselves are only formed on the spill path
+      constexpr uint32_t kSW = kBlock * 4u, kRingB = (uint32_t)RING * kSW, kRingBMask = (uint32_t)kRingMask * kSW;
+      uint32_t sq = 0, sqlim = kRingB;
       bool susp_now = false;   // SUSP: this lane's traversal is parked at the end of this phase
       uint32_t susp_pleaf = kDone;
       if constexpr (SUSP) {
@@ -939,8 +951,8 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
           const unsigned long long w1 = (unsigned long long)__double_as_longlong(a.b);
           cur = (uint32_t)w0;
           susp_pleaf = (uint32_t)(w0 >> 32);
-          sp = (int)(w1 & 0xffffu);
-          slo = (int)((w1 >> 16) & 0x7fffu);
+          sq = (uint32_t)(w1 & 0xffffu) * kSW;
+          sqlim = ((uint32_t)((w1 >> 16) & 0x7fffu) + (uint32_t)RING) * kSW;
           shadow_hit = ((w1 >> 31) & 1ull) != 0ull;
           best = (int)(uint32_t)(w1 >> 32);
           best_slot = (int)(uint32_t)__double_as_longlong(b.a);
@@ -948,22 +960,26 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
           hi_c = round_up_f(tlim - t_off);
         }
       }
+      auto ring = [&](uint32_t q) -> __attribute__((address_space(3))) uint32_t& {
+        return *reinterpret_cast<__attribute__((address_space(3))) uint32_t*>((size_t)((q & kRingBMask) | lane_b));
+      };
       auto push = [&](uint32_t x) {
-        if (sp - slo == RING) {
-          spill[(size_t)slo * P.nslots] = stk[(slo & kRingMask) * kBlock];
-          slo++;
+        if (sq == sqlim) {   // ring full: its bottom entry goes to the spill stack
+          const uint32_t qlo = sqlim - kRingB;
+          spill[(size_t)(qlo / kSW) * P.nslots] = ring(qlo);
+          sqlim += kSW;
           if (STATS) d_spills++;
           if constexpr (TL) tl_spill++;
         }
-        stk[(sp & kRingMask) * kBlock] = x;
-        sp++;
+        ring(sq) = x;
+        sq += kSW;
       };
       auto pop = [&]() -> uint32_t {
-        if (sp == 0) return kDone;
-        --sp;
-        if (sp >= slo) return stk[(sp & kRingMask) * kBlock];
-        slo = sp;
-        return spill[(size_t)sp * P.nslots];
+        if (sq == 0) return kDone;
+        sq -= kSW;
+        if (sq + kRingB >= sqlim) return ring(sq);
+        sqlim = sq + kRingB;
+        return spill[(size_t)(sq / kSW) * P.nslots];
       };
       const D3 c3 = d3(-rd.x, -rd.y, -rd.z);
 
@@ -1068,7 +1084,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
           if (heads_left > 0 && __popcll(__ballot(cur != kDone || pleaf != kDone)) <= kSuspActive) {
             if (cur != kDone || pleaf != kDone) {
               const unsigned long long w0 = (unsigned long long)cur | ((unsigned long long)pleaf << 32);
-              const unsigned long long w1 = (unsigned long long)((uint32_t)sp | ((uint32_t)slo << 16) |
+              const unsigned long long w1 = (unsigned long long)((sq / kSW) | (((sqlim - kRingB) / kSW) << 16) |
                                                                   (shadow_hit ? 0x80000000u : 0u)) |
                                             ((unsigned long long)(uint32_t)best << 32);
               buf_st(prs, pvo, (uint32_t)R_SUSP * kRegionBytes, __longlong_as_double((long long)w0));
@@ -1349,7 +1365,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
           const bool take = idle && r < n;
           if (take) {
             const int t = w * 64 + kth_set_bit(got, r);   // donor thread
-            const uint32_t* ds = lvis + kBlock + t;        // its stack entries
+            const uint32_t* ds = reinterpret_cast<const uint32_t*>(lds_raw) + t;   // its stack entries
             uint32_t v_[kMigWords];
 #pragma unroll
             for (int k = 0; k < kMigWords; ++k) v_[k] = ds[k * kBlock];
@@ -1926,12 +1942,10 @@ inline int variant_ring(int v) { return (v == 4 || v == 5) ? kRingDeep : kShortS
 #ifndef RT_SUSP_MODE
 #define RT_SUSP_MODE 1   // suspend/resume: 0 never, 1 several-frame launches of deep scenes, 2 all launches (A/B)
 #endif
-// LDS per block: kSlotDoubles doubles of slot, task + visibility words and
-// min(stack_words, ring) stack entries per thread.
-size_t lds_bytes(int stack_words, int ring = kShortStack) {
-  stack_words = std::max(stack_words, kMigWords);   // compaction hands registers over in stack entries
-  return (size_t)kBlock *
-         (kSlotDoubles * sizeof(double) + (2 + (size_t)std::min(stack_words, ring)) * sizeof(uint32_t));
+// LDS per block: the variant's stack ring (ring entries per thread, at address 0: the kernel's
+// slot offsets are compile-time constants), kSlotDoubles doubles of slot, task + visibility words.
+size_t lds_bytes(int /*stack_words*/, int ring = kShortStack) {
+  return (size_t)kBlock * (kSlotDoubles * sizeof(double) + (2 + (size_t)ring) * sizeof(uint32_t));
 }
 // ... plus the top treelet (n_top 128-B nodes) after it
 size_t lds_bytes_total(int stack_words, int n_top, int ring = kShortStack) {
