@@ -15,9 +15,10 @@ work queue, so the drain at the end of a launch is paid once per F frames).  The
 F frames of a launch follow an animation path (rtamd.camera_orbit, --sweep): they
 are distinct views, and every frame traces all of its rays.  A single_frame record
 (one frame per launch, the reference's use, mytracer_gpu.cu:59-81; consecutive views of
-the orbit) is timed after the main run, and beside it single_frame.cost_ordered: the same
-launches with RT_FLAG_COST_ORDER (each launch's work heads take the tiles that took
-longest in the previous launch first, shortening the drain).  --streams S > 1 keeps S launches in flight on separate streams
+the orbit) is timed after the main run with the library's default for such launches on one
+stream -- cost-ordered work (each launch's work heads take first the tiles that took longest
+two launches before, shortening the drain) -- and beside it
+single_frame.natural_order: the same launches with RT_FLAG_NATURAL_ORDER.  --streams S > 1 keeps S launches in flight on separate streams
 (default 1 on one GPU: launches serial, so the HIP-event launch duration is the
 kernel's own duration, as rocprofv3 reports it; 2 on N > 1, so the RCCL gather of
 launch i overlaps launch i+1).
@@ -313,8 +314,9 @@ def main():
     last_image = image
 
     # single-frame record: the reference's use, one frame per launch (mytracer_gpu.cu:59-81)
-    # (NS consecutive views of the orbit, one per launch), then the same with RT_FLAG_COST_ORDER: each
-    # launch ordered by the previous launch's per-tile costs (one ordered pass of the NS views first)
+    # (NS consecutive views of the orbit, one per launch) in the natural tile order, then with the
+    # library's default for consecutive one-frame launches on a stream: each launch ordered by the
+    # per-tile costs of the launch two before (one untimed pass of the NS views first)
     single = None
     if a.single_frames > 0 and not a.adaptive:
         def single_record(flags):
@@ -322,9 +324,12 @@ def main():
             el = timed_region(lambda: run(NS, True, per_launch=1, flags=flags))
             return {"frames": NS, "rays_per_frame": None, "ms_per_frame": round(el / NS * 1e3, 4),
                     "kernel_ms_avg": round(float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)])), 4)}
+        natural = single_record(rtamd.abi.RT_FLAG_NATURAL_ORDER)
+        run(NS, False, per_launch=1)
         single = single_record(0)
-        run(NS, False, per_launch=1, flags=rtamd.abi.RT_FLAG_COST_ORDER)
-        single["cost_ordered"] = single_record(rtamd.abi.RT_FLAG_COST_ORDER)
+        single["order"] = ("cost-ordered (library default on one stream)" if S == 1 else
+                           "natural (launches alternate streams)")
+        single["natural_order"] = natural
         single["views"] = "consecutive camera-orbit views, one per launch"
 
     tot = torch.tensor([rays_timed_local, rays_frame0_local, work_bytes_frame], dtype=torch.float64, device="cuda")
@@ -339,7 +344,7 @@ def main():
         ms_per_step = elapsed / a.steps * 1e3
         mrays = rays_total / elapsed / 1e6
         if single is not None:
-            for rec in (single, single["cost_ordered"]):
+            for rec in (single, single["natural_order"]):
                 rec["rays_per_frame"] = int(rays_frame0)
                 rec["value"] = round(rays_frame0 / (rec["ms_per_frame"] * 1e-3) / 1e6, 2)
                 rec["unit"] = "Mrays/s"

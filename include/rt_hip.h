@@ -102,12 +102,17 @@ enum {
   RT_FLAG_TIMELINE = 4,        /* production kernel + per-round timeline (diagnostics, rt_debug_timeline) */
   RT_FLAG_TILE_COST = 8,       /* diagnostics: per-tile cost of the launch (rt_debug_tile_cost): bounces */
   RT_FLAG_TILE_COST_TIME = 16, /* ... the same, as pixel lifetimes (10-ns ticks) */
-  RT_FLAG_COST_ORDER = 32      /* one-frame launches (the reference's use): every work head renders the tiles
-                                  that took longest in the previous RT_FLAG_COST_ORDER launch of the same image
-                                  geometry first (animation: frame i's costs order frame i + 1), and this
-                                  launch's costs are kept for the next; shortens the end-of-launch drain.
-                                  Launches of several frames, or of more than 32768 tiles, keep the natural
-                                  order but still record costs.  Pixels are unchanged */
+  RT_FLAG_COST_ORDER = 32,     /* cost-ordered work for one-frame launches (the reference's use): every work head
+                                  renders first the tiles that took longest (pixel lifetimes) in the launch before
+                                  the previous one of the same image geometry (animation: frame i - 2's costs
+                                  order frame i), and this launch's costs are kept; shortens the end-of-launch
+                                  drain, pixels unchanged.  The DEFAULT for one-frame launches
+                                  that follow the scene's previous launch on the same stream; this flag also
+                                  orders a launch on another stream (it then waits for the previous launch).
+                                  Launches of several frames and adaptive passes keep the natural order and
+                                  record nothing; one-frame launches of more than 32768 tiles (8x8 pixels) keep
+                                  the natural order */
+  RT_FLAG_NATURAL_ORDER = 64   /* one-frame launch in the natural tile order, recording no costs */
 };
 
 /* One render call.  Rows are rendered as interleaved stripes:

@@ -362,6 +362,10 @@ __device__ __forceinline__ float next_down(float f) {
   const uint32_t u = __float_as_uint(f);
   return __uint_as_float(f > 0.0f ? u - 1u : u + 1u);
 }
+// wave ballot of a per-lane predicate (a ballot of a single compare is its mask; of a combined
+// predicate the backend re-materialises it with a v_cndmask + v_cmp pair, so hot loops OR / AND
+// the ballots of the single compares instead)
+__device__ __forceinline__ unsigned long long wballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 __device__ __forceinline__ float round_up_f(double x) {
   float f = (float)x;
   if ((double)f < x) f = next_up(f);
@@ -381,19 +385,19 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
 
 // Counts one wave-level iteration (and its active lanes) on the first active lane.
 __device__ __forceinline__ void wave_tick(unsigned long long& iters, unsigned long long& lanes, int lane) {
-  const unsigned long long m = __ballot(1);
+  const unsigned long long m = wballot(1);
   if (lane == __ffsll((long long)m) - 1) { iters++; lanes += __popcll(m); }
 }
 
 // Adds the number of distinct keys among the active lanes (wave-uniform loop) on the
 // first active lane: distinct lines one load instruction touches, the L1 tag rate's unit.
 __device__ __forceinline__ void wave_distinct(uint32_t key, unsigned long long& acc, int lane) {
-  unsigned long long m = __ballot(1);
+  unsigned long long m = wballot(1);
   const int first = __ffsll((long long)m) - 1;
   unsigned n = 0;
   while (m) {
     const uint32_t k = __shfl(key, __ffsll((long long)m) - 1);
-    m &= ~__ballot(key == k);
+    m &= ~wballot(key == k);
     n++;
   }
   if (lane == first) acc += n;
@@ -657,7 +661,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
   // the first active lane of each iteration charges the time since then to the previous kind
   unsigned long long tl_gsum[4] = {0, 0, 0, 0}, tl_gcnt[4] = {0, 0, 0, 0}, tl_gap = 0;
   auto tl_wave_gap = [&](uint32_t kind) {
-    const unsigned long long m = __ballot(1);
+    const unsigned long long m = wballot(1);
     if (lane == __ffsll((long long)m) - 1) {
       const uint32_t now = (uint32_t)__builtin_amdgcn_s_memrealtime();
       const uint32_t prev = ltask[wbase + 63], pk = ltask[wbase + 62];
@@ -722,8 +726,8 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
     }
     if (STATS) { d_outer++; t_stamp = stamp(); }
     // ---------------- refill idle lanes (one atomic per wave) ----------------
-    unsigned long long m_fetch = __ballot(state == ST_FETCH);
-    unsigned long long m_busy = __ballot(state == ST_CLOSEST || state == ST_SHADOW || state >= ST_HSHADOW);
+    unsigned long long m_fetch = wballot(state == ST_FETCH);
+    unsigned long long m_busy = wballot(state == ST_CLOSEST || state == ST_SHADOW || state >= ST_HSHADOW);
     while (m_fetch && (__popcll(m_fetch) >= kRefill || m_busy == 0) && heads_left > 0) {
       const long long g0 = (n_tiles * head / kGroups) * 64;
       const long long g1 = (n_tiles * (head + 1) / kGroups) * 64;
@@ -788,14 +792,14 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
           }
         }
       }
-      m_fetch = __ballot(state == ST_FETCH);
-      m_busy = __ballot(state == ST_CLOSEST || state == ST_SHADOW || state >= ST_HSHADOW);
+      m_fetch = wballot(state == ST_FETCH);
+      m_busy = wballot(state == ST_CLOSEST || state == ST_SHADOW || state >= ST_HSHADOW);
       if (__popcll(m_fetch) < kRefill && m_busy != 0) break;
     }
     if (heads_left == 0 && state == ST_FETCH) state = ST_DONE;
     const bool busy = (state == ST_CLOSEST || state == ST_SHADOW || state >= ST_HSHADOW);
-    if (__ballot(busy) == 0) {
-      if (__ballot(state != ST_DONE) != 0) continue;
+    if (wballot(busy) == 0) {
+      if (wballot(state != ST_DONE) != 0) continue;
       // every lane done: leave the block's live set.  The last live wave stays while lanes
       // handed over by donors are still pooled (it adopts them below; no traversal runs).
       bool leave = true;
@@ -989,7 +993,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
       // A loop that runs past kTravGuard iterations abandons the ray (results void) and flags
       // the launch.  (Cost: 0.3 % for the node loop, A/B.)
       auto guard_trip = [&]() {
-        if (lane == __ffsll((long long)__ballot(1)) - 1) atomicOr(&P.ctr[CD_GUARD], 1ull);
+        if (lane == __ffsll((long long)wballot(1)) - 1) atomicOr(&P.ctr[CD_GUARD], 1ull);
       };
       // tests the triangles of leaf `lref` in record order; true = any-hit ray occluded
       auto test_leaf = [&](uint32_t lref) -> bool {
@@ -1011,8 +1015,8 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
               c_tris++;
               wave_tick(d_leaf_it, d_leaf_ln, lane);
               wave_distinct((uint32_t)(((unsigned long long)i * sizeof(GTri)) >> 7), d_leaf_lines, lane);
-              const uint32_t i0 = __shfl(i, __ffsll((long long)__ballot(1)) - 1);
-              if (__ballot(i != i0) == 0) wave_tick(d_leaf_uni, d_dummy, lane);
+              const uint32_t i0 = __shfl(i, __ffsll((long long)wballot(1)) - 1);
+              if (wballot(i != i0) == 0) wave_tick(d_leaf_uni, d_dummy, lane);
             }
             const TriOps T = load_tri(P.tris, rec);
             const int slot = (int)(T.meta & kSlotMask);
@@ -1072,7 +1076,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
       }
 
       uint32_t rounds = 0;
-      while (__ballot(cur != kDone || pleaf != kDone) != 0) {
+      while ((wballot(cur != kDone) | wballot(pleaf != kDone)) != 0) {
         if (++rounds > kTravGuard) {   // watchdog: abandon the round (results void, launch flagged)
           guard_trip();
           cur = kDone;
@@ -1081,7 +1085,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
         }
         if constexpr (SUSP) {
           // few lanes left and work to fetch: park the rest, shade and refill, resume next phase
-          if (heads_left > 0 && __popcll(__ballot(cur != kDone || pleaf != kDone)) <= kSuspActive) {
+          if (heads_left > 0 && __popcll(wballot(cur != kDone) | wballot(pleaf != kDone)) <= kSuspActive) {
             if (cur != kDone || pleaf != kDone) {
               const unsigned long long w0 = (unsigned long long)cur | ((unsigned long long)pleaf << 32);
               const unsigned long long w1 = (unsigned long long)((sq / kSW) | (((sqlim - kRingB) / kSW) << 16) |
@@ -1143,7 +1147,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
           float4 nx, fx, ny, fy, nz, fz;
           uint4 rf;
           // wave-uniform: every active lane's node is in the LDS treelet -> ds_read, no TD cost
-          if (__ballot(cur >= (uint32_t)P.n_top) == 0) {
+          if (wballot(cur >= (uint32_t)P.n_top) == 0) {
             if (STATS) wave_tick(d_node_lds, d_dummy, lane);
             if constexpr (TL) tl_wave_gap(2);
             const unsigned char* lb = lds_raw + P.top_off + cur * (uint32_t)sizeof(GNode4);
@@ -1164,8 +1168,8 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
             if constexpr (TL) { tl_gnode++; tl_wave_gap(1); }
             if (STATS) {
               wave_distinct(cur, d_gn_dist, lane);
-              const uint32_t c0 = __shfl(cur, __ffsll((long long)__ballot(1)) - 1);
-              if (__ballot(cur != c0) == 0) wave_tick(d_gn_uni, d_dummy, lane);
+              const uint32_t c0 = __shfl(cur, __ffsll((long long)wballot(1)) - 1);
+              if (wballot(cur != c0) == 0) wave_tick(d_gn_uni, d_dummy, lane);
             }
             nx = *reinterpret_cast<const float4*>(RT_NODE_AT(nxo));
             fx = *reinterpret_cast<const float4*>(RT_NODE_AT(nxo ^ 16u));
@@ -1208,7 +1212,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
             pleaf = cur;
             cur = pop();
           }
-          if (__ballot(pleaf == kDone && cur != kDone) == 0) break;   // every lane holds a leaf
+          if ((wballot(pleaf == kDone) & wballot(cur != kDone)) == 0) break;   // every lane holds a leaf (one mask per compare)
         }
         }
         // leaves: 2-wide -- the leaf the lane stopped at; 4-wide -- the postponed leaf, then
@@ -1261,9 +1265,9 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
         const unsigned long long x = __shfl_xor(gmax, o);
         gmax = x > gmax ? x : gmax;
       }
-      const unsigned nb = (unsigned)__popcll(__ballot(busy));
-      const unsigned no = (unsigned)__popcll(__ballot(state == ST_CLOSEST || state == ST_SHADOW));
-      const unsigned nsh = (unsigned)__popcll(__ballot(busy && (state == ST_SHADOW || state == ST_HSHADOW)));
+      const unsigned nb = (unsigned)__popcll(wballot(busy));
+      const unsigned no = (unsigned)__popcll(wballot(state == ST_CLOSEST || state == ST_SHADOW));
+      const unsigned nsh = (unsigned)__popcll(wballot(busy && (state == ST_SHADOW || state == ST_HSHADOW)));
       if (lane == 0 && tl_n < (unsigned)kTlCap) {
         unsigned long long* r =
             P.tl + kTlWords * ((size_t)(blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * kTlCap + tl_n);
@@ -1302,10 +1306,10 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
       // wave in block, wave-uniform (an SGPR: derived at the use, not a VGPR held across the loop)
       const int wib = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
       const bool owner = (state == ST_CLOSEST || state == ST_SHADOW);
-      const unsigned long long O = __ballot(owner);
+      const unsigned long long O = wballot(owner);
       // (a wave with parked traversals keeps them: their stacks live in its LDS ring entries)
       if (O != 0ull && __popcll(O) <= kDonateMax && *pool_live >= 2u &&
-          (!SUSP || __ballot((state & kSuspBit) != 0) == 0ull)) {
+          (!SUSP || wballot((state & kSuspBit) != 0) == 0ull)) {
         // registers -> this thread's LDS stack entries, then publish the lane mask
         if (owner) {
           // packed: state (3 bits) | shadow hit | frame (< 128) | sample (< 4096) | refl_h + 1 (9 bits);
@@ -1343,7 +1347,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
         if (owner && !((back >> lane) & 1ull)) state = ST_DONE;   // adopted by another wave
       } else {
         // adopt pooled lanes of other waves into idle lanes
-        unsigned long long I = __ballot((state == ST_FETCH || state == ST_DONE) && !refl_held);
+        unsigned long long I = wballot((state == ST_FETCH || state == ST_DONE) && !refl_held);
         for (int w = 0; w < kBlock / 64 && I != 0ull; ++w) {
           if (w == wib || pool_mask[w] == 0ull) continue;
           unsigned long long got = 0ull;
@@ -1392,7 +1396,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
             thit = *R.tlim;   // a closest-hit ray's distance (a shadow batch's owner does not read thit)
             pix_t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
           }
-          I &= ~__ballot(take);
+          I &= ~wballot(take);
         }
       }
       wave_lds_sync();
@@ -1598,12 +1602,12 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
           }
           // one atomic per distinct tile among the lanes finishing here (a wave's lanes mostly share
           // one or two tiles; 64 atomics on one address queue at the memory side)
-          unsigned long long m = __ballot(1);
+          unsigned long long m = wballot(1);
           while (m != 0ull) {
             const int ld = __ffsll((long long)m) - 1;
             const uint32_t tl = (uint32_t)__shfl((int)t, ld);
             const bool same = (uint32_t)t == tl;
-            const unsigned long long ms = __ballot(same);
+            const unsigned long long ms = wballot(same);
             uint32_t sum = same ? c : 0u;
 #pragma unroll
             for (int o = 32; o >= 1; o >>= 1) sum += (uint32_t)__shfl_xor((int)sum, o);
@@ -1644,8 +1648,8 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
     // ---- lend idle lanes to owners' extra rays (extra lights in order, then reflection) ----
     {
       const bool idle = (state == ST_FETCH || state == ST_DONE);
-      const unsigned long long I = __ballot(idle);
-      if (I != 0ull && __ballot(want > 0) != 0ull) {
+      const unsigned long long I = wballot(idle);
+      if (I != 0ull && wballot(want > 0) != 0ull) {
         if (idle) ltask[threadIdx.x] = kTaskNone;
         int incl = want;   // inclusive prefix sum of want over the wave
 #pragma unroll
@@ -1736,18 +1740,25 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
     // the next launch's work order, built by the first blocks to finish (their CUs would idle in the
     // drain): job h < 8 sorts head range h of order_src by cost, descending (stable: equal costs keep
     // the natural band order); jobs 8..15 clear an eighth of zero_map.  The block's LDS is free now.
-    __syncthreads();
+    // A block takes jobs until none is left, so a launch of fewer than 16 blocks (a small image)
+    // still completes all of them (one job per block left the order of the last head ranges stale:
+    // a non-permutation, tiles rendered twice or not at all).
     uint32_t* job = reinterpret_cast<uint32_t*>(lds_raw);
-    if (threadIdx.x == 0) *job = (uint32_t)atomicAdd(&P.ctr[CT_ORDER_JOBS], 1ull);
-    __syncthreads();
-    const uint32_t j = *job;
-    __syncthreads();
-    if (j < (uint32_t)kGroups) {
-      if (P.order_src) order_range(P.order_src, P.next_order, P.n_pos, (int)j, lds_raw);
+    for (;;) {
+      __syncthreads();   // the previous job is done with the LDS
+      if (threadIdx.x == 0) *job = (uint32_t)atomicAdd(&P.ctr[CT_ORDER_JOBS], 1ull);
+      __syncthreads();
+      const uint32_t j = *job;
+      __syncthreads();   // every thread has read it before the sort reuses the LDS
+      if (j >= 2u * kGroups) break;
+      if (j < (uint32_t)kGroups) {
+        if (P.order_src) order_range(P.order_src, P.next_order, P.n_pos, (int)j, lds_raw);
+      } else {
+        for (long long i = P.n_pos * (j - kGroups) / kGroups + threadIdx.x; i < P.n_pos * (j - kGroups + 1) / kGroups;
+             i += kBlock)
+          P.zero_map[i] = 0u;
+      }
     }
-    else if (j < 2u * kGroups)
-      for (long long i = P.n_pos * (j - kGroups) / kGroups + threadIdx.x; i < P.n_pos * (j - kGroups + 1) / kGroups; i += kBlock)
-        P.zero_map[i] = 0u;
   }
 }
 
@@ -1844,7 +1855,7 @@ __global__ void __launch_bounds__(kSelThreads) adaptive_select_kernel(const doub
         }
       }
     }
-    const unsigned long long m = __ballot(sel);
+    const unsigned long long m = wballot(sel);
     if (m != 0ull) {
       const int leader = __ffsll((long long)m) - 1;
       uint32_t base = 0u;
@@ -1999,6 +2010,7 @@ struct rt_scene {
   LaunchCtx ctx[kContexts];
   int next_ctx = 0;             // ring cursor
   int last_ctx = -1;            // context of the most recent launch
+  hipStream_t last_stream = nullptr;   // ... and its stream
   size_t nslots = 0;
   double* d_lights = nullptr;   // [light_cap][6] position xyz, colour rgb
   int light_cap = 0;            // lights d_lights can hold
@@ -2382,7 +2394,16 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   // one of the same geometry, while this launch's costs are recorded
   // (several frames per launch: natural order and no cost map -- the same tile position of every
   // frame finishing together made the cost atomics contend: +57-86 % on 20-frame launches)
-  const bool cost_order = !list && n_frames == 1 && (p->flags & RT_FLAG_COST_ORDER);
+  // The library default for one-frame launches (the reference's use) when they follow each other on
+  // one stream: implicit, so it never adds a cross-stream dependency; explicit RT_FLAG_COST_ORDER
+  // also orders launches on other streams (each then waits for the previous launch's end).
+  // Diagnostics, a debug order and RT_FLAG_NATURAL_ORDER keep the natural order.
+  const bool debug_order = sc->d_tile_order && sc->tile_order_n == P.n_tiles;
+  const bool implicit_order =
+      !(p->flags & (RT_FLAG_TRAVERSAL_STATS | RT_FLAG_WIDE_STATS | RT_FLAG_TIMELINE | RT_FLAG_TILE_COST |
+                    RT_FLAG_TILE_COST_TIME | RT_FLAG_NATURAL_ORDER)) &&
+      !debug_order && (sc->last_ctx < 0 || sc->last_stream == st);
+  const bool cost_order = !list && n_frames == 1 && ((p->flags & RT_FLAG_COST_ORDER) || implicit_order);
   const bool cost_debug = !list && (p->flags & (RT_FLAG_TILE_COST | RT_FLAG_TILE_COST_TIME));
   if (cost_order || cost_debug) {
     const long long n_pos = (long long)P.tiles_x * ((rows + 7) / 8);
@@ -2395,11 +2416,15 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
       for (uint32_t*& q : sc->d_order) HIP_TRY(hipMalloc(reinterpret_cast<void**>(&q), (size_t)n_pos * sizeof(uint32_t)));
       sc->cost_cap = n_pos;
       sc->cost_seq = 0;
+      sc->order_for = -1;
     }
-    if (sc->cost_n != n_pos || sc->cost_tiles_x != P.tiles_x) sc->cost_seq = 0;   // another geometry
+    if (sc->cost_n != n_pos || sc->cost_tiles_x != P.tiles_x) {   // another geometry: a new sequence
+      sc->cost_seq = 0;
+      sc->order_for = -1;   // (an order built for the old geometry is no permutation of this one)
+    }
     sc->cost_n = n_pos;
     sc->cost_tiles_x = P.tiles_x;
-    if (sc->last_ctx >= 0)   // the previous launch (any stream) has finished with the maps
+    if (sc->last_ctx >= 0 && sc->last_stream != st)   // the previous launch (another stream) is done with the maps
       HIP_TRY(hipStreamWaitEvent(st, sc->ctx[sc->last_ctx].ev1, 0));
     // cost unit: pixel lifetime (RT_FLAG_TILE_COST_TIME, and RT_FLAG_COST_ORDER alone) or bounces
     // (RT_FLAG_TILE_COST, also with RT_FLAG_COST_ORDER)
@@ -2415,7 +2440,7 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
       if (q == 0)
         for (uint32_t* m : sc->d_cost) HIP_TRY(hipMemsetAsync(m, 0, (size_t)n_pos * sizeof(uint32_t), st));
       P.tile_cost = sc->d_cost[q % 3];
-      if (sc->order_for == q) {
+      if (sc->order_for == q && n_pos == P.n_tiles) {
         P.tile_order = sc->d_order[q % 2];
         sc->last_order_n = P.n_tiles;
         sc->last_order_buf = (int)(q % 2);
@@ -2492,6 +2517,7 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   C.variant = v;
   C.waves = rows > 0 ? blocks * (kBlock / 64) : 0;
   sc->last_ctx = ci;
+  sc->last_stream = st;
   sc->next_ctx = (ci + 1) % kContexts;
   if (stats) {
     HIP_TRY(hipStreamSynchronize(st));

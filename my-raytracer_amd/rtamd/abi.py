@@ -24,6 +24,7 @@ RT_FLAG_TIMELINE = 4
 RT_FLAG_TILE_COST = 8
 RT_FLAG_TILE_COST_TIME = 16
 RT_FLAG_COST_ORDER = 32
+RT_FLAG_NATURAL_ORDER = 64
 
 
 class Material(C.Structure):

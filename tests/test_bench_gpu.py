@@ -54,7 +54,7 @@ def test_bench_json_contract_and_saved_frame(tmp_path, frames):
     assert rf["frac"] is None or 0.0 < rf["frac"] <= 1.0
     sf = d["single_frame"]
     assert sf["frames"] == min(16, frames) and sf["ms_per_frame"] > 0 and sf["value"] > 0
-    co = sf["cost_ordered"]
+    co = sf["natural_order"]
     assert co["frames"] == sf["frames"] and co["ms_per_frame"] > 0 and co["rays_per_frame"] == sf["rays_per_frame"]
     ref, rays = expected_frames(320, 180, frames)
     assert np.array_equal(np.load(out), ref)

@@ -237,6 +237,18 @@ def test_tile_order_and_costs_change_no_pixel(nf):
         lib.rt_debug_tile_cost(dev._h, cost.ctypes.data_as(C.POINTER(C.c_uint)), n)
         assert cost.min() > 0
     if nf == 1:   # the ordered launches used a permutation of the tiles
+        # (and plain one-frame launches on the same stream are cost-ordered by default: they record
+        # their costs too; RT_FLAG_NATURAL_ORDER records nothing and leaves the last map as it was)
+        img, c = render(0)
+        assert all(np.array_equal(a, b) for a, b in zip(img, ref)) and c == rc
+        cost = np.zeros(25 * 15, dtype=np.uint32)
+        lib.rt_debug_tile_cost(dev._h, cost.ctypes.data_as(C.POINTER(C.c_uint)), cost.size)
+        assert cost.min() > 0
+        img, c = render(rtamd.abi.RT_FLAG_NATURAL_ORDER)
+        assert all(np.array_equal(a, b) for a, b in zip(img, ref)) and c == rc
+        again = np.zeros_like(cost)
+        lib.rt_debug_tile_cost(dev._h, again.ctypes.data_as(C.POINTER(C.c_uint)), again.size)
+        assert np.array_equal(again, cost)
         m = lib.rt_debug_last_tile_order(dev._h, None, 0)
         assert m == n_tiles
         got = np.zeros(m, dtype=np.uint32)
@@ -250,6 +262,31 @@ def test_tile_order_and_costs_change_no_pixel(nf):
     bad[0] = n_tiles
     assert lib.rt_debug_set_tile_order(dev._h, bad.ctypes.data_as(C.POINTER(C.c_uint)), n_tiles) != 0
     assert lib.rt_debug_set_tile_order(dev._h, None, 0) == 0
+
+
+@pytest.mark.parametrize("size", [(40, 30), (16, 8), (200, 113)])
+def test_default_cost_order_small_launches(size):
+    # One-frame launches on one stream are cost-ordered by default, the order for launch i built in
+    # the drain of launch i - 1.  Launches of fewer blocks than order jobs (16) must still complete
+    # every job: each ordered launch equals the natural-order render, bit for bit.
+    w, h = size
+    hs, dev, _ = Case.get("cornell")
+    p = hs.render_params(w, h, 1)
+    p.out_format = rtamd.RT_OUT_RGB_F64
+    q = rtamd.abi.RenderParams.from_buffer_copy(p)
+    q.flags = rtamd.abi.RT_FLAG_NATURAL_ORDER
+    frames = [_moved(p, 0.02 * f) for f in range(6)]
+    for f in frames:
+        ref, _ = dev.render(_with_flags(f, rtamd.abi.RT_FLAG_NATURAL_ORDER))
+        for _ in range(3):   # the sequence continues across frames: ordered from its third launch on
+            img, _ = dev.render(f)
+            assert np.array_equal(img, ref)
+
+
+def _with_flags(p, flags):
+    q = rtamd.abi.RenderParams.from_buffer_copy(p)
+    q.flags = flags
+    return q
 
 
 def test_concurrent_launches_on_streams_are_independent():

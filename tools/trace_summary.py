@@ -6,10 +6,10 @@ usage: python tools/trace_summary.py OUT.json PROF_DIR BENCH.json
 bench.py's production-kernel dispatches come in a fixed order: the counting launch of F frames
 (plus one of steps % F frames when F does not divide --steps), the counting launch of the NS
 single-frame views, the warm-up launches, the timed launches, then three runs of NS one-frame
-launches: the single-frame record, an untimed RT_FLAG_COST_ORDER pass, and the cost-ordered
-record.  The summary averages the timed launches and each single-frame record separately, so each
-figure can be set beside the bench's own HIP-event kernel_ms_avg / single_frame.kernel_ms_avg /
-single_frame.cost_ordered.kernel_ms_avg.
+launches: the natural-order record, an untimed pass in the library's default (cost) order, and
+the default-order single-frame record.  The summary averages the timed launches and each
+single-frame record separately, so each figure can be set beside the bench's own HIP-event
+kernel_ms_avg / single_frame.kernel_ms_avg / single_frame.natural_order.kernel_ms_avg.
 """
 import csv
 import glob
@@ -40,8 +40,8 @@ def main():
     n_single = bench["single_frame"]["frames"] if bench.get("single_frame") else 0
     t0 = n_count + n_warm
     timed = dur[t0:t0 + n_timed]
-    single = dur[t0 + n_timed:t0 + n_timed + n_single]
-    ordered = dur[t0 + n_timed + 2 * n_single:t0 + n_timed + 3 * n_single]
+    natural = dur[t0 + n_timed:t0 + n_timed + n_single]
+    single = dur[t0 + n_timed + 2 * n_single:t0 + n_timed + 3 * n_single]
     sf = bench.get("single_frame") or {}
     res = {
         "production_dispatches": len(dur),
@@ -52,9 +52,9 @@ def main():
         "single_frame_launches": len(single),
         "single_ms_avg": sum(single) / len(single) if single else None,
         "bench_single_kernel_ms_avg": sf.get("kernel_ms_avg"),
-        "cost_ordered_launches": len(ordered),
-        "cost_ordered_ms_avg": sum(ordered) / len(ordered) if ordered else None,
-        "bench_cost_ordered_kernel_ms_avg": (sf.get("cost_ordered") or {}).get("kernel_ms_avg"),
+        "natural_order_launches": len(natural),
+        "natural_order_ms_avg": sum(natural) / len(natural) if natural else None,
+        "bench_natural_order_kernel_ms_avg": (sf.get("natural_order") or {}).get("kernel_ms_avg"),
         "all_ms": [round(d, 4) for d in dur],
         "source": os.path.normpath(pdir),
     }
