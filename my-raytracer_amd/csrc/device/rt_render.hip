@@ -499,15 +499,19 @@ __device__ __forceinline__ uint32_t u4c(const uint4& v, int c) {
 // out of work, from the cost map of the launch before, so it costs no launch and no busy CU.
 constexpr int kOrderItems = 16;
 constexpr long long kOrderMaxRange = (long long)kBlock * kOrderItems;   // tiles per head range (4096)
-// Sort keys: an 8-bit log-scale cost class (16 per octave, 2^8 .. 2^24 ticks) inverted so that higher
-// costs sort first, above the 12-bit local index; one radix pass over the class bits (stable).
+// Sort keys: a log-scale cost class (4 per octave from 2^8 ticks; 16 per octave: -1.5 %, 1 per
+// octave: +-0, profiles/r03/r03u_ab_order_*.txt) inverted so that higher costs sort first, above the
+// 12-bit local index; one radix pass over the 8 class bits (stable: equal classes keep band order).
+#ifndef RT_ORDER_SHIFT
+#define RT_ORDER_SHIFT 21   // cost classes per octave: 2^(23 - RT_ORDER_SHIFT)
+#endif
 __device__ __forceinline__ uint32_t order_class(uint32_t cost) {
-  const int q = (int)(__float_as_uint((float)cost) >> 19) - ((127 + 8) << 4);
+  const int q = (int)(__float_as_uint((float)cost) >> RT_ORDER_SHIFT) - ((127 + 8) << (23 - RT_ORDER_SHIFT));
   return 255u - (uint32_t)min(255, max(0, q));
 }
 __device__ void order_range(const uint32_t* cost, uint32_t* order, long long n_tiles, int h, unsigned char* lds) {
   using Sort = rocprim::block_radix_sort<unsigned int, kBlock, kOrderItems>;
-  static_assert(sizeof(typename Sort::storage_type) <= 32768, "sort storage must fit the block's LDS");
+  static_assert(sizeof(typename Sort::storage_type) <= 30720, "sort storage must fit the block's LDS (at least 30 KB)");
   auto& storage = *reinterpret_cast<typename Sort::storage_type*>(lds);
   const long long t0 = n_tiles * h / kGroups, t1 = n_tiles * (h + 1) / kGroups;
   unsigned int keys[kOrderItems];

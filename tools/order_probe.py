@@ -122,8 +122,8 @@ for nf in (1, F):
             m = lib.rt_debug_last_tile_order(dev._h, None, 0)
             got = np.zeros(m, dtype=np.uint32)
             lib.rt_debug_last_tile_order(dev._h, got.ctypes.data_as(C.POINTER(C.c_uint)), m)
-            # the library sorts 8-bit log-scale cost classes (16 per octave), stable
-            q = np.clip((cpos.astype(np.float32).view(np.uint32) >> 19).astype(np.int64) - ((127 + 8) << 4), 0, 255)
+            # the library sorts 8-bit log-scale cost classes (4 per octave, RT_ORDER_SHIFT 21), stable
+            q = np.clip((cpos.astype(np.float32).view(np.uint32) >> 21).astype(np.int64) - ((127 + 8) << 2), 0, 255)
             want = order_from_costs(q.astype(np.uint32), "desc")
             print(f"   library order == host exact order: {np.array_equal(got, want)} "
                   f"(first differences at {np.nonzero(got != want)[0][:5]})", flush=True)

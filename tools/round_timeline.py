@@ -17,6 +17,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("scene", nargs="?", default="office")
 ap.add_argument("tris", nargs="?", type=int, default=0)
 ap.add_argument("--depth", type=int, default=-1)
+ap.add_argument("--order", action="store_true", help="cost-ordered launches (RT_FLAG_COST_ORDER), warmed up")
 a = ap.parse_args()
 host = rtamd.HostScene.generate(a.scene, **({"n_triangles": a.tris} if a.tris else {}))
 host.prepare()
@@ -32,10 +33,12 @@ p = host.render_params(1920, 1080, 1)
 if a.depth >= 0:
     p.max_depth = a.depth
 ms = []
+base = rtamd.abi.RT_FLAG_COST_ORDER if a.order else rtamd.abi.RT_FLAG_NATURAL_ORDER
+p.flags = base
 for _ in range(5):
     gpu.launch(p, out.data_ptr())
     ms.append(gpu.last_kernel_ms())
-p.flags = rtamd.RT_FLAG_TIMELINE
+p.flags = rtamd.RT_FLAG_TIMELINE | (rtamd.abi.RT_FLAG_COST_ORDER if a.order else 0)
 gpu.launch(p, out.data_ptr())
 gpu.launch(p, out.data_ptr())
 tl_ms = gpu.last_kernel_ms()
@@ -66,6 +69,8 @@ print(f"  round us {pct(dur[u])}; busy {pct(busy[u])}; lane iters {pct(iters[u])
 T = float(np.nanmax(end))
 t_end = np.nanmax(end, axis=1)[waves]
 print(f"  wave end us {pct(t_end, (0, 10, 50, 90, 100))}")
+qd = start[used & (queued == 0)]
+print(f"  queue empty from {np.nanmin(qd) if len(qd) else float('nan'):.0f} us (first round that saw no work left) of {T:.0f} us")
 # time per wave-level iteration by kind, in time windows (round start)
 edges = [0, 100, 200, 300, 400, 500, 600, 700, 10_000]
 print("  us per wave-level iteration by kind and round-start window (count):")
