@@ -316,6 +316,41 @@ __device__ __forceinline__ D3 normalize(D3 v) {
   if (n > 0.0) return D3{v.x / n, v.y / n, v.z / n};
   return v;
 }
+#ifndef RT_FAST_SHADE
+#define RT_FAST_SHADE 3   // A/B: bit 0 normalize_shade, bit 1 pow_shade
+#endif
+#define RT_NORM_SHADE(v) ((RT_FAST_SHADE & 1) ? normalize_shade(v) : normalize(v))
+#define RT_POW_SHADE(x, y) ((RT_FAST_SHADE & 2) ? pow_shade(x, y) : pow(x, y))
+// Shading-only helpers for the specular term (never a ray, never a branch that switches a term on or
+// off): results within a few ulp of the reference's sqrt-and-divide normalisation and libm pow --
+// far inside the fp64 parity tolerance (1e-12), while everything that defines a ray (camera, shadow
+// and reflection directions, the triangle test) or decides a branch keeps the reference's exact
+// operations.
+// normalize: v_rsq_f64 + one Newton step and three multiplies instead of a sqrt and three divisions.
+__device__ __forceinline__ D3 normalize_shade(D3 v) {
+  const double q = dot(v, v);
+  if (!(q > 1e-200 && q < 1e200)) return normalize(v);   // zero, tiny, huge or NaN: the exact path
+  const double r0 = __builtin_amdgcn_rsq(q);
+  const double e = __builtin_fma(-(q * r0), r0, 1.0);   // 1 - q r0^2
+  const double r = __builtin_fma(0.5 * r0, e, r0);
+  return D3{v.x * r, v.y * r, v.z * r};
+}
+// pow for the Phong highlight: integer exponents 1 .. 256 (the usual material exponents) by binary
+// powering (relative error below 2^8 ulp for x in [0, 1]), others through pow.
+__device__ __forceinline__ double pow_shade(double x, double y) {
+  if (y >= 1.0 && y <= 256.0 && y == __builtin_floor(y)) {
+    uint32_t n = (uint32_t)y;
+    double r = 1.0, b = x;
+    for (;;) {
+      if (n & 1u) r *= b;
+      n >>= 1;
+      if (n == 0u) break;
+      b *= b;
+    }
+    return r;
+  }
+  return pow(x, y);
+}
 __device__ __forceinline__ double stdmax(double a, double b) { return (a < b) ? b : a; }
 __device__ __forceinline__ double stdmin(double a, double b) { return (b < a) ? b : a; }
 
@@ -1416,16 +1451,16 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
       // lighting() for one light (mytracer.cpp:579-606): Lambert + Phong term of light j
       auto contrib_of = [&](int j, D3 hp_, D3 hn_, D3 hv_, D3 hd_, const GMat& M) {
         const Light6 L6 = light_of(j);
-        const D3 l = normalize(sub(L6.pos, hp_));
+        const D3 l = normalize(sub(L6.pos, hp_));   // exact: it decides diff > 0 (a discontinuity)
         const double diff = stdmax(0.0, dot(hn_, l));
         double refl = 0.0;
         if (diff > 0.0) {   // reflection(), mytracer.cpp:524-534
           const double s2 = 2.0 * dot(hn_, l);
-          const D3 r = normalize(sub(scl(s2, hn_), l));
+          const D3 r = RT_NORM_SHADE(sub(scl(s2, hn_), l));   // feeds only max(0, r.v)^shininess: continuous
           refl = stdmax(0.0, dot(r, hv_));
         }
         // pow(+0, y > 0) = +0 exactly: skip the fp64 pow for the (frequent) zero highlight
-        if (!(refl == 0.0 && M.shininess > 0.0)) refl = pow(refl, M.shininess);
+        if (!(refl == 0.0 && M.shininess > 0.0)) refl = RT_POW_SHADE(refl, M.shininess);
         return d3(L6.col.x * (hd_.x * diff + M.ks[0] * refl), L6.col.y * (hd_.y * diff + M.ks[1] * refl),
                   L6.col.z * (hd_.z * diff + M.ks[2] * refl));
       };

@@ -2,12 +2,11 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out
-T=r03q
-bash tools/gpu_r03.sh ${T} || exit $?
-B="python -u bench.py --no-cpu-baseline"
-for v in new prev new prev; do
-  L=my-raytracer_amd/lib/librt_hip.so; [ $v != new ] && L=my-raytracer_amd/lib/variants/librt_hip_$v.so
-  RTAMD_HIP_LIB=$L timeout -k 10 300 $B >> $O/${T}_office_$v.jsonl 2> $O/${T}_office_$v.err || exit $?
-  RTAMD_HIP_LIB=$L timeout -k 10 300 $B --steps 20 --warmup 5 >> $O/${T}_drv_$v.jsonl 2> $O/${T}_drv_$v.err || exit $?
-done
-echo done
+V=my-raytracer_amd/lib/variants
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+  > $O/fs_gpu_tests.txt 2>&1 || { tail -40 $O/fs_gpu_tests.txt; exit 1; }
+tail -1 $O/fs_gpu_tests.txt
+bash tools/ab.sh 3 "" $V/librt_hip_fs0.so $V/librt_hip_fs1.so $V/librt_hip_fs2.so $V/librt_hip_fs3.so > $O/ab_fs_office.txt || exit 1
+cat $O/ab_fs_office.txt
+bash tools/ab.sh 2 "--scene random_tris --tris 10000000 --single-frames 0" $V/librt_hip_fs0.so $V/librt_hip_fs3.so > $O/ab_fs_rt10m.txt || exit 1
+cat $O/ab_fs_rt10m.txt
