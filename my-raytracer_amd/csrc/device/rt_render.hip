@@ -319,6 +319,9 @@ __device__ __forceinline__ D3 normalize(D3 v) {
 #ifndef RT_FAST_SHADE
 #define RT_FAST_SHADE 3   // A/B: bit 0 normalize_shade, bit 1 pow_shade
 #endif
+#ifndef RT_MED3_WINDOW
+#define RT_MED3_WINDOW 1   // A/B: the node loop's t-window bound through med3 (no per-iteration canonicalize)
+#endif
 #define RT_NORM_SHADE(v) ((RT_FAST_SHADE & 1) ? normalize_shade(v) : normalize(v))
 #define RT_POW_SHADE(x, y) ((RT_FAST_SHADE & 2) ? pow_shade(x, y) : pow(x, y))
 // Shading-only helpers for the specular term (never a ray, never a branch that switches a term on or
@@ -976,6 +979,8 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
       const float oix = ofx * ivx, oiy = ofy * ivy, oiz = ofz * ivz;
       const float lo_c = round_down_f(-t_off);
       float hi_c = round_up_f(tlim - t_off);
+      float pinf = INFINITY;   // opaque to the combiner: a constant med3 operand folds back to min / max
+      asm volatile("" : "+s"(pinf));
       // logical stack [0, sp); the LDS ring holds [slo, sp), spill[] holds [0, slo).  Kept byte-scaled
       // by a lane's ring stride (kSW = kBlock words, in bytes): sq = sp * kSW, sqlim = (slo + RING) * kSW, so a
       // push is one compare with sqlim, one AND-OR for the ring address (the lane's byte offset sits
@@ -1224,8 +1229,16 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
             const float tx0 = __builtin_fmaf(f4c(nx, c), ivx, -oix), tx1 = __builtin_fmaf(f4c(fx, c), ivx, -oix);
             const float ty0 = __builtin_fmaf(f4c(ny, c), ivy, -oiy), ty1 = __builtin_fmaf(f4c(fy, c), ivy, -oiy);
             const float tz0 = __builtin_fmaf(f4c(nz, c), ivz, -oiz), tz1 = __builtin_fmaf(f4c(fz, c), ivz, -oiz);
+            // the window bound enters through med3 (med3(t, lo, +inf) = max, med3(t, hi, -inf) = min;
+            // no operand is ever NaN: |inv| <= 1e20, finite or empty-box planes): fminf / fmaxf of
+            // the loop-carried bound made the compiler re-canonicalise it every iteration (2 VALU)
+#if RT_MED3_WINDOW
+            const float tn = fmaxf(fmaxf(tx0, ty0), __builtin_amdgcn_fmed3f(tz0, lo_c, pinf));
+            const float tf = fminf(fminf(tx1, ty1), __builtin_amdgcn_fmed3f(tz1, hi_c, -pinf));
+#else
             const float tn = fmaxf(fmaxf(tx0, ty0), fmaxf(tz0, lo_c));
             const float tf = fminf(fminf(tx1, ty1), fminf(tz1, hi_c));
+#endif
             const uint32_t r = u4c(rf, c);
             const bool h = tn <= tf;   // absent children carry the empty box [+inf, -inf]
             k[c] = h ? tn : INFINITY;
