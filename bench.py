@@ -62,6 +62,9 @@ HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # The CU's vector-L1 data return (TD): one 64-lane dwordx4 wave-instruction per 16 cycles =
 # 64 B/clk/CU (tools/l1_micro.hip) x 256 CUs x 2.4 GHz.
 L1_PEAK_GBPS = 64 * 256 * 2.4
+# VALU issue: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 4 cycles per SIMD (16 lanes per cycle,
+# fp32, fp64 and integer alike) at 2.4 GHz -- in wave-level instructions per second
+VALU_PEAK_GINSTS = 256 * 4 * 2.4 / 4
 STRIPE_H = 16
 
 
@@ -379,6 +382,7 @@ def main():
                         "def": "128*wide_node_visits + 80*tri_tests + 96*closest_hits (production kernel) / "
                                "(64 B/clk x 256 CUs x 2.4 GHz)"},
             "wave_cycles": pmc_wave_mix(workload_key(a, n), frames_per_launch),
+            "valu_roof": pmc_valu_roof(workload_key(a, n), frames_per_launch, kernel_s / frames_per_launch),
         })
         out = {
             "metric": "Mrays/sec (primary+shadow+reflect), Office 1920x1080 1spp",
@@ -512,6 +516,36 @@ def pmc_wave_mix(key, frames_per_launch=None):
                                    same_round[0])
     return {"issue_frac": round(issue, 3), "mem_wait_frac": round(wait, 3),
             "other_frac": round(1.0 - issue - wait, 3), "source": str(path.relative_to(ROOT))}
+
+
+def pmc_valu_roof(key, frames_per_launch, kernel_s_per_frame):
+    """The resource that binds the render kernel: VALU issue.  achieved = wave-level
+    VALU instructions per frame (rocprofv3 SQ_INSTS_VALU of this workload, newest committed summary,
+    as pmc_per_frame picks it) / this run's kernel time per frame, against VALU_PEAK_GINSTS;
+    busy_frac = SQ_ACTIVE_INST_VALU (quad-cycles) x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs) of
+    the profiled run itself.  None when no such pass was committed."""
+    cands = []
+    for path, d in _newest_first(key):
+        try:
+            insts = d["SQ_INSTS_VALU"]["per_frame"]
+        except (KeyError, TypeError):
+            continue
+        busy = None
+        try:
+            busy = d["SQ_ACTIVE_INST_VALU"]["per_frame"] * 4 / (1024 * d["GRBM_GUI_ACTIVE"]["per_frame"] / 8)
+        except (KeyError, TypeError, ZeroDivisionError):
+            pass
+        cands.append((_profile_tag(path), path, d, insts, busy))
+    if not cands:
+        return None
+    same_round = [c for c in cands if c[0] == cands[0][0]]
+    _, path, d, insts, busy = next((c for c in same_round if frames_per_launch is not None
+                                    and c[2].get("_bench", {}).get("frames_per_launch") == frames_per_launch),
+                                   same_round[0])
+    achieved = insts / kernel_s_per_frame / 1e9
+    return {"unit": "G wave-instr/s", "achieved": round(achieved, 1), "peak": round(VALU_PEAK_GINSTS, 1),
+            "frac": round(achieved / VALU_PEAK_GINSTS, 4), "valu_insts_per_frame": int(insts),
+            "busy_frac": round(busy, 4) if busy is not None else None, "source": str(path.relative_to(ROOT))}
 
 
 def usable_cpus():

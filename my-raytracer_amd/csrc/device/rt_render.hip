@@ -316,6 +316,33 @@ __device__ __forceinline__ D3 normalize(D3 v) {
   if (n > 0.0) return D3{v.x / n, v.y / n, v.z / n};
   return v;
 }
+#ifndef RT_SHARED_RCP
+#define RT_SHARED_RCP 1   // A/B: normalize() with one reciprocal for its three divisions
+#endif
+// normalize: the same sqrt, then x / n for each component -- with ONE refined reciprocal of n for
+// the three divisions.  The compiler's correctly rounded fp64 division is
+//   d0 = div_scale(n), r = rcp(d0), r = fma(r, fma(-d0, r, 1), r) twice, q = d1 * r,
+//   q = div_fmas(fma(-d0, q, d1), r, q), div_fixup(q, n, x)
+// and div_scale / div_fixup are identities when no operand is zero, denormal or near an exponent
+// limit and the quotient cannot over- or underflow: here every |component| in [2^-200, 2^200]
+// (so n in [2^-200, 2^201]).  Inside that range this is the same sequence of operations on the same
+// operands with the reciprocal steps done once, so the result is bit-identical to normalize_div;
+// outside it (a zero component included) normalize runs.  (Production variants only: in the
+// diagnostic ones the extra live ranges spill.)
+__device__ __forceinline__ D3 normalize_rcp(D3 v) {
+  if (!RT_SHARED_RCP) return normalize(v);
+  const double ax = fabs(v.x), ay = fabs(v.y), az = fabs(v.z);
+  const bool ok = ax >= 0x1p-200 && ax <= 0x1p200 && ay >= 0x1p-200 && ay <= 0x1p200 && az >= 0x1p-200 &&
+                  az <= 0x1p200;
+  if (!ok) return normalize(v);
+  const double n = sqrt(dot(v, v));
+  double r = __builtin_amdgcn_rcp(n);
+  r = __builtin_fma(r, __builtin_fma(-n, r, 1.0), r);
+  r = __builtin_fma(r, __builtin_fma(-n, r, 1.0), r);
+  const double qx = v.x * r, qy = v.y * r, qz = v.z * r;
+  return D3{__builtin_fma(__builtin_fma(-n, qx, v.x), r, qx), __builtin_fma(__builtin_fma(-n, qy, v.y), r, qy),
+            __builtin_fma(__builtin_fma(-n, qz, v.z), r, qz)};
+}
 #ifndef RT_FAST_SHADE
 #define RT_FAST_SHADE 3   // A/B: bit 0 normalize_shade, bit 1 pow_shade
 #endif
@@ -733,9 +760,14 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
     return Light6{d3(L[0], L[1], L[2]), d3(L[3], L[4], L[5])};
   };
 
+  // normalize(): one shared reciprocal in the production variants (bit-identical, normalize_rcp)
+  auto nrm = [](D3 v) -> D3 {
+    if constexpr (STATS || TL) return normalize(v);
+    else return normalize_rcp(v);
+  };
   // Ray(o, d): stores origin, normalised direction and t-limit to the LDS slot.
   auto emit_ray = [&](D3 o, D3 dir, double t_limit) {
-    const D3 d = normalize(dir);
+    const D3 d = nrm(dir);
     *R.o[0] = o.x; *R.o[1] = o.y; *R.o[2] = o.z;
     *R.d[0] = d.x; *R.d[1] = d.y; *R.d[2] = d.z;
     *R.tlim = t_limit;
@@ -895,9 +927,9 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
         const int j = (state == ST_SHADOW) ? light : (int)((htask >> 11) & 0xFFFFFu);
         const D3 hp = add(ro, scl(tlim, rd));
         const D3 to_l = sub(light_of(j).pos, hp);
-        const D3 l = normalize(to_l);
+        const D3 l = nrm(to_l);
         ro = add(hp, scl(1e-4, l));
-        rd = normalize(l);
+        rd = nrm(l);
         tlim = sqrt(dot(to_l, to_l));
       } else if (state == ST_HCLOSEST) {
         // the owner's reflection ray (mytracer.cpp:547-552), from its hit and its normal (the
@@ -907,7 +939,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
         const double s2 = 2.0 * dot(hn, rd);   // reflect(d, n) = d - 2(n.d)n, d = -view = rd
         const D3 v = sub(rd, scl(s2, hn));
         ro = add(hp, scl(1e-4, v));
-        rd = normalize(v);
+        rd = nrm(v);
         tlim = DBL_MAX;
         *R.o[0] = ro.x; *R.o[1] = ro.y; *R.o[2] = ro.z;
         *R.d[0] = rd.x; *R.d[1] = rd.y; *R.d[2] = rd.z;
@@ -964,7 +996,15 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
         for (int k = 0; k < 3; ++k) {
           float df = (float)d3v[k];
           if (fabsf(df) < 1e-20f) df = signbit(d3v[k]) ? -1e-20f : 1e-20f;
-          inv[k] = 1.0f / df;
+          if constexpr (WIDTH == 4 && RT_SHARED_RCP) {
+            // v_rcp_f32 (1 ulp) + one Newton step: within about half an ulp of 1 / df, as the
+            // correctly rounded division (11 VALU) it replaces; the box error bound of DESIGN.md
+            // §4 stays far inside delta.  (The 2-wide canonical kernel keeps the oracle's division.)
+            const float r0 = __builtin_amdgcn_rcpf(df);
+            inv[k] = __builtin_fmaf(__builtin_fmaf(-df, r0, 1.0f), r0, r0);
+          } else {
+            inv[k] = 1.0f / df;
+          }
         }
       }
       const float ofx = (float)(ro.x + t_off * rd.x);
@@ -1464,7 +1504,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
       // lighting() for one light (mytracer.cpp:579-606): Lambert + Phong term of light j
       auto contrib_of = [&](int j, D3 hp_, D3 hn_, D3 hv_, D3 hd_, const GMat& M) {
         const Light6 L6 = light_of(j);
-        const D3 l = normalize(sub(L6.pos, hp_));   // exact: it decides diff > 0 (a discontinuity)
+        const D3 l = nrm(sub(L6.pos, hp_));   // exact: it decides diff > 0 (a discontinuity)
         const double diff = stdmax(0.0, dot(hn_, l));
         double refl = 0.0;
         if (diff > 0.0) {   // reflection(), mytracer.cpp:524-534
