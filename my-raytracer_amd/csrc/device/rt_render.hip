@@ -326,22 +326,55 @@ __device__ __forceinline__ D3 normalize(D3 v) {
 // and div_scale / div_fixup are identities when no operand is zero, denormal or near an exponent
 // limit and the quotient cannot over- or underflow: here every |component| in [2^-200, 2^200]
 // (so n in [2^-200, 2^201]).  Inside that range this is the same sequence of operations on the same
-// operands with the reciprocal steps done once, so the result is bit-identical to normalize_div;
-// outside it (a zero component included) normalize runs.  (Production variants only: in the
-// diagnostic ones the extra live ranges spill.)
-__device__ __forceinline__ D3 normalize_rcp(D3 v) {
-  if (!RT_SHARED_RCP) return normalize(v);
-  const double ax = fabs(v.x), ay = fabs(v.y), az = fabs(v.z);
-  const bool ok = ax >= 0x1p-200 && ax <= 0x1p200 && ay >= 0x1p-200 && ay <= 0x1p200 && az >= 0x1p-200 &&
-                  az <= 0x1p200;
-  if (!ok) return normalize(v);
-  const double n = sqrt(dot(v, v));
+// operands with the reciprocal steps done once, so the result is bit-identical to normalize;
+// outside it (a zero component included) normalize runs.  n = |v| is returned too (the shadow ray's
+// light distance is that same sqrt).  (Production variants only: in the diagnostic ones the extra
+// live ranges spill.)
+#ifndef RT_FAST_SQRT
+#define RT_FAST_SQRT 1   // A/B: sqrt of a guarded normal argument without the scaling / class fix-ups
+#endif
+#ifndef RT_TRI_RCP
+#define RT_TRI_RCP 0     // A/B: the triangle test's three divisions by S with one reciprocal (-0.9 %, off)
+#endif
+// sqrt of q >= 2^-767, finite: the compiler's fp64 sqrt expansion is "scale q up by 2^256 if below
+// 2^-767, v_rsq_f64 + two Newton refinements, scale back, return q itself for +-0 / +inf"; for such
+// q the scaling and the fix-up are identities, and this is the rest of it -- the same operations in
+// the same order, bit-identical to sqrt(q).
+__device__ __forceinline__ double sqrt_normal(double q) {
+  if (!RT_FAST_SQRT) return sqrt(q);
+  const double y = __builtin_amdgcn_rsq(q);
+  double g = q * y, h = y * 0.5;
+  const double r = __builtin_fma(-h, g, 0.5);
+  g = __builtin_fma(g, r, g);
+  double d = __builtin_fma(-g, g, q);
+  h = __builtin_fma(h, r, h);
+  g = __builtin_fma(d, h, g);
+  d = __builtin_fma(-g, g, q);
+  return __builtin_fma(d, h, g);
+}
+// the refined reciprocal of the compiler's fp64 division x / n (see above), and one quotient with it
+__device__ __forceinline__ double rcp_refined(double n) {
   double r = __builtin_amdgcn_rcp(n);
   r = __builtin_fma(r, __builtin_fma(-n, r, 1.0), r);
-  r = __builtin_fma(r, __builtin_fma(-n, r, 1.0), r);
-  const double qx = v.x * r, qy = v.y * r, qz = v.z * r;
-  return D3{__builtin_fma(__builtin_fma(-n, qx, v.x), r, qx), __builtin_fma(__builtin_fma(-n, qy, v.y), r, qy),
-            __builtin_fma(__builtin_fma(-n, qz, v.z), r, qz)};
+  return __builtin_fma(r, __builtin_fma(-n, r, 1.0), r);
+}
+__device__ __forceinline__ double div_by(double x, double n, double r) {
+  const double q = x * r;
+  return __builtin_fma(__builtin_fma(-n, q, x), r, q);
+}
+// |x| in [2^-300, 2^300]: quotients of two such values need neither div_scale nor div_fixup
+__device__ __forceinline__ bool div_safe(double x) { return fabs(x) >= 0x1p-300 && fabs(x) <= 0x1p300; }
+__device__ __forceinline__ D3 normalize_rcp(D3 v, double& n) {
+  const double ax = fabs(v.x), ay = fabs(v.y), az = fabs(v.z);
+  const bool ok = RT_SHARED_RCP && ax >= 0x1p-200 && ax <= 0x1p200 && ay >= 0x1p-200 && ay <= 0x1p200 &&
+                  az >= 0x1p-200 && az <= 0x1p200;
+  if (!ok) {
+    n = sqrt(dot(v, v));
+    return normalize(v);
+  }
+  n = sqrt_normal(dot(v, v));
+  const double r = rcp_refined(n);
+  return D3{div_by(v.x, n, r), div_by(v.y, n, r), div_by(v.z, n, r)};
 }
 #ifndef RT_FAST_SHADE
 #define RT_FAST_SHADE 3   // A/B: bit 0 normalize_shade, bit 1 pow_shade
@@ -761,9 +794,17 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
   };
 
   // normalize(): one shared reciprocal in the production variants (bit-identical, normalize_rcp)
-  auto nrm = [](D3 v) -> D3 {
-    if constexpr (STATS || TL) return normalize(v);
-    else return normalize_rcp(v);
+  auto nrm_n = [](D3 v, double& n) -> D3 {
+    if constexpr (STATS || TL) {
+      n = sqrt(dot(v, v));
+      return normalize(v);
+    } else {
+      return normalize_rcp(v, n);
+    }
+  };
+  auto nrm = [&](D3 v) -> D3 {
+    double n;
+    return nrm_n(v, n);
   };
   // Ray(o, d): stores origin, normalised direction and t-limit to the LDS slot.
   auto emit_ray = [&](D3 o, D3 dir, double t_limit) {
@@ -776,10 +817,17 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
   // primary ray of the current sample (mytracer_gpu.cu:202-209; Camera::primary_ray)
   auto start_sample = [&]() {
     const int n = P.spp_n;
-    const int si = sample / n, sj = sample - si * n;
-    const double xo = (si) / (double)n - 0.5 + 1.0 / (2.0 * n);
-    const double yo = (sj) / (double)n - 0.5 + 1.0 / (2.0 * n);
-    const double X = (double)px + xo, Y = (double)py + yo;
+    double X, Y;
+    if (RT_SHARED_RCP && n == 1) {   // xo = 0/1 - 0.5 + 1/2 = +0 exactly: X = px + 0 = px
+      X = (double)px;
+      Y = (double)py;
+    } else {
+      const int si = sample / n, sj = sample - si * n;
+      const double xo = (si) / (double)n - 0.5 + 1.0 / (2.0 * n);
+      const double yo = (sj) / (double)n - 0.5 + 1.0 / (2.0 * n);
+      X = (double)px + xo;
+      Y = (double)py + yo;
+    }
     const FrameDesc& K = P.frames[frame];
     const D3 dir = d3(K.ll[0] + X * K.xd[0] + Y * K.yd[0] - K.eye[0],
                       K.ll[1] + X * K.xd[1] + Y * K.yd[1] - K.eye[1],
@@ -927,10 +975,11 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
         const int j = (state == ST_SHADOW) ? light : (int)((htask >> 11) & 0xFFFFFu);
         const D3 hp = add(ro, scl(tlim, rd));
         const D3 to_l = sub(light_of(j).pos, hp);
-        const D3 l = nrm(to_l);
+        double nl;   // |to_l|: the light distance, the same sqrt as the normalisation's
+        const D3 l = nrm_n(to_l, nl);
         ro = add(hp, scl(1e-4, l));
         rd = nrm(l);
-        tlim = sqrt(dot(to_l, to_l));
+        tlim = nl;
       } else if (state == ST_HCLOSEST) {
         // the owner's reflection ray (mytracer.cpp:547-552), from its hit and its normal (the
         // owner's aux words); kept in this helper's slot, from which the owner takes it over
@@ -1120,11 +1169,27 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
               const bool out = (ua < 0.0 && -ua >= tiny) || (ub < 0.0 && -ub >= tiny) || ua > big || ub > big ||
                                (Da + Db - S) * sS > 0x1p-40 * (fabs(Da) + fabs(Db) + aS);
               if (!out) {
-                const double t = det3(T.e1, T.e2, c4) / S;
+                const double Dt = det3(T.e1, T.e2, c4);
+                // the three quotients by S with one reciprocal where that is bit-identical (div_safe)
+                const bool fdiv = RT_TRI_RCP && !STATS && !TL && div_safe(S) && div_safe(Dt) && div_safe(Da) &&
+                                  div_safe(Db);
+                double rS = 0.0, t;
+                if (fdiv) {
+                  rS = rcp_refined(S);
+                  t = div_by(Dt, S, rS);
+                } else {
+                  t = Dt / S;
+                }
                 const bool cand = anyhit ? (t < tlim) : (t <= tlim);
                 if (t > 1e-5 && cand) {
-                  const double alpha = Da / S;
-                  const double beta = Db / S;
+                  double alpha, beta;
+                  if (fdiv) {
+                    alpha = div_by(Da, S, rS);
+                    beta = div_by(Db, S, rS);
+                  } else {
+                    alpha = Da / S;
+                    beta = Db / S;
+                  }
                   const double gamma = (1.0 - alpha - beta);
                   const bool inside = (0.0 <= alpha && alpha <= 1.0) && (0.0 <= beta && beta <= 1.0) &&
                                       (0.0 <= gamma && gamma <= 1.0);
