@@ -164,6 +164,33 @@ __device__ __forceinline__ D2 buf_ld2(__amdgpu_buffer_rsrc_t r, uint32_t voff, u
 // (no b128 store helper: path-state stores are b64, see ST4 in render_kernel)
 
 
+#ifndef RT_DPP_SCAN
+#define RT_DPP_SCAN 0   // A/B: fan-out prefix sum by DPP row shifts / broadcasts instead of __shfl_up (+-0.5 %, off)
+#endif
+// Inclusive prefix sum over the wave's 64 lanes (all lanes active): DPP row_shr 1, 2, 4, 8 within each
+// 16-lane row, then row_bcast:15 (rows 1, 3 add the last lane of the row below) and row_bcast:31 (rows
+// 2, 3 add lane 31) -- six VALU instead of six ds_bpermute round trips.  Lanes a DPP source does not
+// reach (outside the row, or rows the row mask leaves out) add the `old` operand, 0.
+__device__ __forceinline__ int wave_incl_scan(int x) {
+  if (!RT_DPP_SCAN) {
+    int incl = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(incl, o);
+      if ((int)(threadIdx.x & 63) >= o) incl += v;
+    }
+    return incl;
+  }
+  int v = x;
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);   // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);   // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);   // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);   // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);   // row_bcast:15
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);   // row_bcast:31
+  return v;
+}
+
 // Lane of the k-th (0-based) set bit of m (k < popcount(m)).
 __device__ __forceinline__ int kth_set_bit(unsigned long long m, int k) {
   int base = 0;
@@ -330,6 +357,9 @@ __device__ __forceinline__ D3 normalize(D3 v) {
 // outside it (a zero component included) normalize runs.  n = |v| is returned too (the shadow ray's
 // light distance is that same sqrt).  (Production variants only: in the diagnostic ones the extra
 // live ranges spill.)
+#ifndef RT_IDLE_LIST
+#define RT_IDLE_LIST 0   // A/B: fan-out reads helpers from a ranked idle-lane list (no kth_set_bit; +-0.5 %, off)
+#endif
 #ifndef RT_FAST_SQRT
 #define RT_FAST_SQRT 1   // A/B: sqrt of a guarded normal argument without the scaling / class fix-ups
 #endif
@@ -1808,12 +1838,13 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
       const unsigned long long I = wballot(idle);
       if (I != 0ull && wballot(want > 0) != 0ull) {
         if (idle) ltask[threadIdx.x] = kTaskNone;
-        int incl = want;   // inclusive prefix sum of want over the wave
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          const int v = __shfl_up(incl, o);
-          if (lane >= o) incl += v;
-        }
+#if RT_IDLE_LIST
+        // the idle lanes by rank, in entry 0 of the wave's stack-ring row (free between traversals:
+        // tail compaction's words were read before SHADE, and the SUSP variants, which park stacks in
+        // the ring, lend no lanes): an owner's t-th helper is one LDS read instead of a bit search
+        if (idle) reinterpret_cast<uint32_t*>(lds_raw)[wbase + __popcll(I & lane_below)] = (uint32_t)lane;
+#endif
+        const int incl = wave_incl_scan(want);   // inclusive prefix sum of want over the wave
         wave_lds_sync();
         const int off = incl - want;
         const int avail = (int)__popcll(I);   // __popcll is unsigned: keep the subtraction signed
@@ -1821,7 +1852,11 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
         if (got > 0) {
           const int n_extra_lights = min(P.n_lights - light - 1, kBatchExtra);
           for (int t = 0; t < got; ++t) {   // task words only: each helper derives its own ray
+#if RT_IDLE_LIST
+            const int ht = wbase + (int)reinterpret_cast<const uint32_t*>(lds_raw)[wbase + off + t];
+#else
             const int ht = wbase + kth_set_bit(I, off + t);
+#endif
             uint32_t tw;
             if (t < n_extra_lights) {
               tw = (uint32_t)lane | ((uint32_t)(t + 1) << 6) | ((uint32_t)(light + 1 + t) << 11);
