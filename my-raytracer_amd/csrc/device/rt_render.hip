@@ -1811,7 +1811,14 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
           int n2 = P.spp_n * P.spp_n;
           asm volatile("" : "+s"(n2));   // converted here, not hoisted into a VGPR live across the loop
           const double nn = (double)n2;
-          const double r = stdmin(pcol.x / nn, 1.0), g = stdmin(pcol.y / nn, 1.0), b = stdmin(pcol.z / nn, 1.0);
+          double r, g, b;
+          if (RT_SHARED_RCP && (n2 & (n2 - 1)) == 0) {
+            // n2 = 2^k: x / n2 = x * 2^-k exactly (one rounding of the same exact value), no division
+            const double s = __builtin_ldexp(1.0, -__builtin_ctz((unsigned)n2));
+            r = stdmin(pcol.x * s, 1.0); g = stdmin(pcol.y * s, 1.0); b = stdmin(pcol.z * s, 1.0);
+          } else {
+            r = stdmin(pcol.x / nn, 1.0); g = stdmin(pcol.y / nn, 1.0); b = stdmin(pcol.z / nn, 1.0);
+          }
           const size_t o = 3 * ((size_t)lrow * P.W + px);
           // nontemporal (evict-first): the frame is written once and never read here, so its lines
           // should not push the path-state lines out of L2 (office: HBM writes 50.9 -> 45.5 MB per
