@@ -1,16 +1,6 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-O=gpurun_out
-V=my-raytracer_amd/lib/variants
-RTAMD_HIP_LIB=$V/librt_hip_prev.so timeout -k 10 300 python -u tools/bitcmp.py $O/bc_base.npz > $O/bc_base.txt 2>&1 || { tail $O/bc_base.txt; exit 1; }
-RTAMD_HIP_LIB=$V/librt_hip_new.so timeout -k 10 300 python -u tools/bitcmp.py $O/bc_all.npz > $O/bc_all.txt 2>&1 || { tail $O/bc_all.txt; exit 1; }
-python tools/bitcmp_diff.py $O/bc_base.npz $O/bc_all.npz | tee $O/bc_diff4.txt
-rm -f $O/bc_base.npz $O/bc_all.npz
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
-  > $O/fin_gpu_tests.txt 2>&1 || { tail -40 $O/fin_gpu_tests.txt; exit 1; }
-tail -1 $O/fin_gpu_tests.txt
-timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/fin_smoke.txt 2>&1 || { tail $O/fin_smoke.txt; exit 1; }
-tail -1 $O/fin_smoke.txt
-bash tools/ab_single.sh 3 "" $V/librt_hip_prev.so $V/librt_hip_new.so > $O/ab_fin_office.txt || exit 1
-cat $O/ab_fin_office.txt
+export CALIB=profiles/r02/hbm_calib.json
+bash tools/configs_bench.sh r03z || exit 1
+bash tools/profile_round.sh rt10m_r03z --scene random_tris --tris 10000000 || exit 1
