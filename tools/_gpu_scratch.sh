@@ -2,6 +2,15 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out
-timeout -k 10 300 python -u tools/diag_probe.py office > $O/r03zc_diag_office.txt 2>&1 || { tail $O/r03zc_diag_office.txt; exit 1; }
-timeout -k 10 300 python -u tools/diag_probe.py random_tris 1920 1080 1 10000000 > $O/r03zc_diag_rt10m.txt 2>&1 || { tail $O/r03zc_diag_rt10m.txt; exit 1; }
-cat $O/r03zc_diag_office.txt $O/r03zc_diag_rt10m.txt
+V=my-raytracer_amd/lib/variants
+RTAMD_HIP_LIB=$V/librt_hip_prev.so timeout -k 10 300 python -u tools/bitcmp.py $O/bc_base.npz > $O/bc_base.txt 2>&1 || { tail $O/bc_base.txt; exit 1; }
+RTAMD_HIP_LIB=$V/librt_hip_bo.so timeout -k 10 300 python -u tools/bitcmp.py $O/bc_all.npz > $O/bc_all.txt 2>&1 || { tail $O/bc_all.txt; exit 1; }
+python tools/bitcmp_diff.py $O/bc_base.npz $O/bc_all.npz | tee $O/bc_diff5.txt
+rm -f $O/bc_base.npz $O/bc_all.npz
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+  > $O/bo_gpu_tests.txt 2>&1 || { tail -40 $O/bo_gpu_tests.txt; exit 1; }
+tail -1 $O/bo_gpu_tests.txt
+bash tools/ab_single.sh 3 "" $V/librt_hip_prev.so $V/librt_hip_bo.so > $O/ab_bo_office.txt || exit 1
+cat $O/ab_bo_office.txt
+bash tools/ab.sh 2 "--scene random_tris --tris 10000000 --single-frames 0" $V/librt_hip_prev.so $V/librt_hip_bo.so > $O/ab_bo_rt10m.txt || exit 1
+cat $O/ab_bo_rt10m.txt
