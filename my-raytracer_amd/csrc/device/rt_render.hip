@@ -363,6 +363,9 @@ __device__ __forceinline__ D3 normalize(D3 v) {
 #ifndef RT_FAST_SQRT
 #define RT_FAST_SQRT 1   // A/B: sqrt of a guarded normal argument without the scaling / class fix-ups
 #endif
+#ifndef RT_AB_RCP
+#define RT_AB_RCP 1      // A/B: the barycentric quotients Da / S, Db / S with one reciprocal
+#endif
 #ifndef RT_TRI_RCP
 #define RT_TRI_RCP 0     // A/B: the triangle test's three divisions by S with one reciprocal (-0.9 %, off)
 #endif
@@ -395,14 +398,15 @@ __device__ __forceinline__ double div_by(double x, double n, double r) {
 // |x| in [2^-300, 2^300]: quotients of two such values need neither div_scale nor div_fixup
 __device__ __forceinline__ bool div_safe(double x) { return fabs(x) >= 0x1p-300 && fabs(x) <= 0x1p300; }
 __device__ __forceinline__ D3 normalize_rcp(D3 v, double& n) {
-  const double ax = fabs(v.x), ay = fabs(v.y), az = fabs(v.z);
-  const bool ok = RT_SHARED_RCP && ax >= 0x1p-200 && ax <= 0x1p200 && ay >= 0x1p-200 && ay <= 0x1p200 &&
-                  az >= 0x1p-200 && az <= 0x1p200;
+  // every |component| >= 2^-200 and |v|^2 <= 2^400 (so every |component| <= 2^200); NaN / inf fail
+  const double q = dot(v, v);
+  const bool ok = RT_SHARED_RCP && fabs(v.x) >= 0x1p-200 && fabs(v.y) >= 0x1p-200 && fabs(v.z) >= 0x1p-200 &&
+                  q <= 0x1p400;
   if (!ok) {
-    n = sqrt(dot(v, v));
+    n = sqrt(q);
     return normalize(v);
   }
-  n = sqrt_normal(dot(v, v));
+  n = sqrt_normal(q);
   const double r = rcp_refined(n);
   return D3{div_by(v.x, n, r), div_by(v.y, n, r), div_by(v.z, n, r)};
 }
@@ -1213,7 +1217,18 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
                 const bool cand = anyhit ? (t < tlim) : (t <= tlim);
                 if (t > 1e-5 && cand) {
                   double alpha, beta;
-                  if (fdiv) {
+                  // alpha, beta: one reciprocal of S for the two quotients where that is bit-identical:
+                  // |S| >= 1e-10 here and |Da|, |Db| <= |S|(1 + 2^-48) (the early rejections), so with
+                  // |Da|, |Db| >= |S| 2^-900 and |S| < 2^1000 no operand or quotient is denormal, zero or
+                  // near an exponent limit (RT_AB_RCP; RT_TRI_RCP shares t's division as well)
+                  const double lim = aS * 0x1p-900;
+                  const bool fab = RT_AB_RCP && !STATS && !TL && !fdiv && fabs(Da) >= lim && fabs(Db) >= lim &&
+                                   aS < 0x1p1000;
+                  if (fab) {
+                    const double r = rcp_refined(S);
+                    alpha = div_by(Da, S, r);
+                    beta = div_by(Db, S, r);
+                  } else if (fdiv) {
                     alpha = div_by(Da, S, rS);
                     beta = div_by(Db, S, rS);
                   } else {
