@@ -996,3 +996,40 @@ def test_fuzz_textured_scene_matches_oracle(tmp_path, seed):
     assert np.abs(img - ref).max() <= TOL64
     assert counts(st) == [cnt.primary_rays, cnt.shadow_rays, cnt.reflection_rays]
     dev.close()
+
+
+def test_axis_aligned_scene_exact_zero_components(tmp_path):
+    # Camera, mirror and lights on the axes, even image size: the centre column / row of primary
+    # rays, the shadow rays to lights straight above hit points and the mirror's reflections have
+    # direction components that are exactly 0 -- the inputs where the kernel's shared-reciprocal
+    # normalize and guarded sqrt hand over to the compiler's full fp64 expansions (§4).  Both paths
+    # must give the oracle's pixels and ray counts.  Mesh extents are deliberately not round: with
+    # the floor edge at x = -3 a 2x2-spp sample ray of the 64x48 image meets the floor exactly on
+    # that edge, where the reference's fp64 slab test (mybvh.cpp:99-135, not conservative) rounds
+    # the leaf box out while the triangle test accepts the edge -- the kernel's conservative boxes
+    # find that hit, as a brute-force renderer does (edge-exact hits).
+    import minirt
+    floor_v = [(-3.07, -1.0, 3.11), (2.93, -1.0, 3.11), (2.93, -1.0, -2.97), (-3.07, -1.0, -2.97)]
+    wall_v, wall_t = kat_scenes.quad(-2.81, 3.13, -1.0, 2.87, -2.0)
+    box_v = [(-0.53, -1.0, 0.0), (0.47, -1.0, 0.0), (0.47, 0.11, 0.0), (-0.53, 0.11, 0.0)]
+    meshes = [minirt.Mesh(floor_v, [(0, 1, 2), (0, 2, 3)], "FLAT", kat_scenes.FLAT_MAT),
+              minirt.Mesh(wall_v, wall_t, "FLAT", kat_scenes.MIRROR_MAT),
+              minirt.Mesh(box_v, [(0, 1, 2), (0, 2, 3)], "FLAT", kat_scenes.FLAT_MAT)]
+    lights = [((0.0, 2.5, 0.0), (0.7, 0.7, 0.7)), ((0.0, 0.0, 3.0), (0.3, 0.3, 0.3))]
+    for w, h in [(16, 12), (64, 48)]:
+        path = tmp_path / f"axis_{w}.sce"
+        minirt.write_sce(path, meshes, lights, ((0.0, 0.0, 4.0), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 50.0, w, h),
+                         (0.05, 0.1, 0.2), (0.2, 0.2, 0.2), 3)
+        hs = rtamd.HostScene.load(path)
+        hs.prepare()
+        orc = pyoracle.Oracle(hs.raw, hs)
+        for spp in (1, 2):
+            p = hs.render_params(0, 0, spp)
+            ref, cnt = orc.render(p, pyoracle.MODE_REFERENCE)
+            p.out_format = rtamd.RT_OUT_RGB_F64
+            dev = rtamd.DeviceScene(hs, 0)
+            img, st = dev.render(p)
+            assert np.abs(img - ref).max() <= TOL64
+            assert counts(st) == [cnt.primary_rays, cnt.shadow_rays, cnt.reflection_rays]
+            assert cnt.reflection_rays > 0 and cnt.shadow_rays > 0
+            dev.close()
