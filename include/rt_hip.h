@@ -192,8 +192,9 @@ typedef struct rt_upload_options {
   int lds_treelet;       /* 4-wide nodes each block caches in LDS: < 0 = as many as fit (default),
                             else at most this many */
   int collapse;          /* RT_COLLAPSE_* (default RT_COLLAPSE_GREEDY) */
-  int sbvh_leaf_max;     /* SBVH: SAH-terminated leaves of up to this many references (default 2;
-                            1 = split down to single references), 1..8 */
+  int sbvh_leaf_max;     /* SBVH: SAH-terminated leaves of up to this many references, 1..8 (1 = split
+                            down to single references); 0 = by size (default): 1 from 2^18 input
+                            triangles on, else 2 */
   int sbvh_bins;         /* SBVH: spatial bins per axis (default 32), 2..128 */
   int blocks_per_cu;     /* persistent blocks per CU: 0 = as many as fit (default), else at most this many */
   int grid_spare;        /* block slots of the persistent grid left free for concurrent kernels (default 0) */

@@ -416,7 +416,11 @@ constexpr double kSbvhBudget = 0.75;     // at most this many extra references p
 // SAH-terminated leaves of up to 2 references (node visit = 1 triangle test): office +3.9 %
 // (15707 -> 16324 Mrays/s, A/B), 4K 16 spp +4.1 %, random triangles -2 %; 3 / 4 references or
 // node costs 0.3 / 2 / 4 lose 0.3-6 %
-constexpr int kSbvhLeafMax = 2;
+// SAH leaf termination (leaves of up to 2 references): office +3.9 %, 4K 16 spp +4.1 %; random
+// triangle soups prefer single-reference leaves (config 4, 10 M: +4.8 %, profiles/r03/r03zh_ab_rt10m_tree.txt).
+// 0 = by size: 1 from kSbvhLeafBySize input triangles on (the size that also selects the 16-entry ring), else 2.
+constexpr int kSbvhLeafMax = 0;
+constexpr long long kSbvhLeafBySize = 1ll << 18;
 
 struct SRef { uint32_t slot; V3 lo, hi; };
 
@@ -729,7 +733,8 @@ void build_sbvh_tree(const rt_scene_soa* s, const rt_upload_options& opt, DevTre
     for (auto& x : th) x.join();
   }
   SbvhCtx C{s, opt.sbvh_alpha, 0.0, std::max(2, std::min(kSbvhBinsMax, opt.sbvh_bins)),
-            std::max(1, std::min(8, opt.sbvh_leaf_max)), opt.sbvh_c_trav};
+            opt.sbvh_leaf_max > 0 ? std::min(8, opt.sbvh_leaf_max) : ((long long)nt >= kSbvhLeafBySize ? 1 : 2),
+            opt.sbvh_c_trav};
   const double budget_frac = opt.sbvh_budget;
   {
     V3 lo = kV3Lo, hi = kV3Hi;
