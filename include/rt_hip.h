@@ -177,7 +177,7 @@ int rt_scene_upload(const rt_scene_soa* soa, const rt_bvh_soa* bvh, int device, 
 enum { RT_TREE_SAH = 0, RT_TREE_REFERENCE = 1, RT_TREE_SBVH = 2 };
 /* 4-wide collapse of the device hierarchy: open the child with the largest box (default), or
  * the SAH-optimal choice of up to 4 slots per node (dynamic programme). */
-enum { RT_COLLAPSE_GREEDY = 0, RT_COLLAPSE_SAH = 1 };
+enum { RT_COLLAPSE_GREEDY = 0, RT_COLLAPSE_SAH = 1, RT_COLLAPSE_BY_SIZE = 2 };
 
 /* Upload options.  The library reads nothing from the environment: its behaviour depends only
  * on these fields and the call's arguments.  Fill with rt_upload_options_init (the defaults),
@@ -191,7 +191,8 @@ typedef struct rt_upload_options {
                             device records on, else 8; default), 8 or 16 */
   int lds_treelet;       /* 4-wide nodes each block caches in LDS: < 0 = as many as fit (default),
                             else at most this many */
-  int collapse;          /* RT_COLLAPSE_* (default RT_COLLAPSE_GREEDY) */
+  int collapse;          /* RT_COLLAPSE_* (default RT_COLLAPSE_BY_SIZE: SAH from 2^18 input triangles on,
+                            else greedy) */
   int sbvh_leaf_max;     /* SBVH: SAH-terminated leaves of up to this many references, 1..8 (1 = split
                             down to single references); 0 = by size (default): 1 from 2^18 input
                             triangles on, else 2 */
@@ -200,8 +201,10 @@ typedef struct rt_upload_options {
   int grid_spare;        /* block slots of the persistent grid left free for concurrent kernels (default 0) */
   int verbose;           /* 1: build phase times to stderr (default 0) */
   double sbvh_alpha;     /* SBVH: try spatial splits where the best object split's children overlap by
-                            more than alpha x the root's surface area (default 1e-5) */
-  double sbvh_budget;    /* SBVH: at most this many extra references per triangle (default 0.75) */
+                            more than alpha x the root's surface area; < 0 = by size (default):
+                            0 from 2^18 input triangles on, else 1e-5 */
+  double sbvh_budget;    /* SBVH: at most this many extra references per triangle; < 0 = by size
+                            (default): 1.5 from 2^18 input triangles on, else 0.75 */
   double sbvh_c_trav;    /* SBVH: node visit cost in triangle tests, for leaf termination (default 1.0) */
   double collapse_c_tri; /* RT_COLLAPSE_SAH: cost of a leaf slot per unit area (default 1.0) */
   int reserved_[8];

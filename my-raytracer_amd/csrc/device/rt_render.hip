@@ -2410,7 +2410,8 @@ int resolve_options(const rt_upload_options* opt, rt_upload_options& o) {
   if (o.blocks_per_cu < 0 || o.grid_spare < 0 || o.build_threads < 0)
     return fail(RT_ERR_INVALID, "rt_scene_upload: negative blocks_per_cu / grid_spare / build_threads");
   if (o.sbvh_leaf_max < 0 || o.sbvh_leaf_max > 8 || o.sbvh_bins < 2 || o.sbvh_bins > 128 ||
-      !(o.sbvh_alpha >= 0.0) || !(o.sbvh_budget >= 0.0) || !(o.sbvh_c_trav >= 0.0) || !(o.collapse_c_tri >= 0.0))
+      o.sbvh_alpha != o.sbvh_alpha || o.sbvh_budget != o.sbvh_budget ||   // NaN; negative = by size
+       !(o.sbvh_c_trav >= 0.0) || !(o.collapse_c_tri >= 0.0))
     return fail(RT_ERR_INVALID, "rt_scene_upload: SBVH / collapse parameter out of range");
   return RT_OK;
 }

@@ -733,8 +733,7 @@ void build_sbvh_tree(const rt_scene_soa* s, const rt_upload_options& opt, DevTre
     for (auto& x : th) x.join();
   }
   SbvhCtx C{s, opt.sbvh_alpha, 0.0, std::max(2, std::min(kSbvhBinsMax, opt.sbvh_bins)),
-            opt.sbvh_leaf_max > 0 ? std::min(8, opt.sbvh_leaf_max) : ((long long)nt >= kSbvhLeafBySize ? 1 : 2),
-            opt.sbvh_c_trav};
+            std::max(1, std::min(8, opt.sbvh_leaf_max)), opt.sbvh_c_trav};
   const double budget_frac = opt.sbvh_budget;
   {
     V3 lo = kV3Lo, hi = kV3Hi;
@@ -873,8 +872,23 @@ int validate(const rt_scene_soa* s, const rt_bvh_soa* b) {
 
 }  // namespace
 
-int build_image(const rt_scene_soa* s, const rt_bvh_soa* b, const rt_upload_options& opt, int bfs_top,
+// Options left "by size" (the defaults) resolved for a scene of nt input triangles: from
+// kSbvhLeafBySize triangles on (random soups, config 4) single-reference leaves, the SAH-optimal
+// collapse and spatial splits wherever they pay (alpha 0, budget 1.5): 10 M random triangles
+// 4722 -> 4804 Mrays/s for the last three (profiles/r03/r03zl_ab_rt10m_tree.txt); below it the
+// office's tuning (leaves of up to 2, greedy collapse, alpha 1e-5, budget 0.75).
+static rt_upload_options options_by_size(rt_upload_options o, long long nt) {
+  const bool deep = nt >= kSbvhLeafBySize;
+  if (o.sbvh_leaf_max == 0) o.sbvh_leaf_max = deep ? 1 : 2;
+  if (o.collapse == RT_COLLAPSE_BY_SIZE) o.collapse = deep ? RT_COLLAPSE_SAH : RT_COLLAPSE_GREEDY;
+  if (o.sbvh_alpha < 0.0) o.sbvh_alpha = deep ? 0.0 : kSbvhAlpha;
+  if (o.sbvh_budget < 0.0) o.sbvh_budget = deep ? 1.5 : kSbvhBudget;
+  return o;
+}
+
+int build_image(const rt_scene_soa* s, const rt_bvh_soa* b, const rt_upload_options& opt_in, int bfs_top,
                 SceneImage& I) {
+  const rt_upload_options opt = options_by_size(opt_in, s ? s->n_vertex_idx / 3 : 0);
   const int tree_kind = opt.device_tree;
   if (tree_kind != RT_TREE_SAH && tree_kind != RT_TREE_REFERENCE && tree_kind != RT_TREE_SBVH)
     return fail(RT_ERR_INVALID, "rt_scene_upload: unknown device_tree");
@@ -1225,14 +1239,14 @@ void upload_options_defaults(rt_upload_options* o) {
   o->build_threads = 0;
   o->stack_ring = 0;
   o->lds_treelet = -1;
-  o->collapse = RT_COLLAPSE_GREEDY;
+  o->collapse = RT_COLLAPSE_BY_SIZE;
   o->sbvh_leaf_max = kSbvhLeafMax;
   o->sbvh_bins = kSbvhBins;
   o->blocks_per_cu = 0;
   o->grid_spare = 0;
   o->verbose = 0;
-  o->sbvh_alpha = kSbvhAlpha;
-  o->sbvh_budget = kSbvhBudget;
+  o->sbvh_alpha = -1.0;    // by size
+  o->sbvh_budget = -1.0;   // by size
   o->sbvh_c_trav = 1.0;
   o->collapse_c_tri = 1.0;
 }

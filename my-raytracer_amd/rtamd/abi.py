@@ -147,7 +147,7 @@ class UploadOptions(C.Structure):
 
 
 RT_TREE_SAH, RT_TREE_REFERENCE, RT_TREE_SBVH = 0, 1, 2
-RT_COLLAPSE_GREEDY, RT_COLLAPSE_SAH = 0, 1
+RT_COLLAPSE_GREEDY, RT_COLLAPSE_SAH, RT_COLLAPSE_BY_SIZE = 0, 1, 2
 
 # Symbols each library must export (declared in include/*.h).
 HIP_SYMBOLS = {

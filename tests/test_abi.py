@@ -79,14 +79,14 @@ def test_upload_options_defaults_and_validation():
     # The library reads no environment: every build / layout choice is an rt_upload_options field.
     o = abi.UploadOptions()
     rtamd.hip_lib().rt_upload_options_init(C.byref(o))
-    assert (o.device_tree, o.stack_ring, o.lds_treelet, o.collapse) == (abi.RT_TREE_SBVH, 0, -1, abi.RT_COLLAPSE_GREEDY)
+    assert (o.device_tree, o.stack_ring, o.lds_treelet, o.collapse) == (abi.RT_TREE_SBVH, 0, -1, abi.RT_COLLAPSE_BY_SIZE)
     assert (o.sbvh_leaf_max, o.sbvh_bins, o.blocks_per_cu, o.grid_spare, o.verbose) == (0, 32, 0, 0, 0)
-    assert (o.sbvh_alpha, o.sbvh_budget, o.sbvh_c_trav, o.collapse_c_tri) == (1e-5, 0.75, 1.0, 1.0)
+    assert (o.sbvh_alpha, o.sbvh_budget, o.sbvh_c_trav, o.collapse_c_tri) == (-1.0, -1.0, 1.0, 1.0)
     hs = rtamd.HostScene.generate("cornell")
     hs.prepare()
     lib = rtamd.hip_lib()
     for field, bad in (("stack_ring", 12), ("blocks_per_cu", -1), ("sbvh_bins", 1), ("sbvh_leaf_max", 9), ("sbvh_leaf_max", -1),
-                       ("device_tree", 7), ("collapse", 3), ("sbvh_alpha", float("nan"))):
+                       ("device_tree", 7), ("collapse", 3), ("sbvh_alpha", float("nan")), ("sbvh_budget", float("nan"))):
         q = rtamd.upload_options(**{field: bad})
         rc = lib.rt_scene_upload_ex(hs.soa, hs.bvh, 0, C.byref(q), C.byref(C.c_void_p()))
         assert rc == abi.RT_ERR_INVALID, (field, rc)
