@@ -62,9 +62,13 @@ HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # The CU's vector-L1 data return (TD): one 64-lane dwordx4 wave-instruction per 16 cycles =
 # 64 B/clk/CU (tools/l1_micro.hip) x 256 CUs x 2.4 GHz.
 L1_PEAK_GBPS = 64 * 256 * 2.4
-# VALU issue: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 4 cycles per SIMD (16 lanes per cycle,
-# fp32, fp64 and integer alike) at 2.4 GHz -- in wave-level instructions per second
-VALU_PEAK_GINSTS = 256 * 4 * 2.4 / 4
+# VALU issue (MI355X_MICROARCH.md, "Per-instruction cycle constants"): a SIMD-32 issues a 32-bit
+# wave64 VALU instruction in 2 cycles (4 cycles is what ONE wave alone sustains), an fp64 one in 4
+# (16 lanes per cycle: 78.6 TF fp64 = half the fp32 rate), a transcendental in 8 (the issue-cost
+# row); 1024 SIMDs at 2.4 GHz.  valu_roof prices each class by its own cycles.
+VALU_SIMDS = 256 * 4
+VALU_CLOCK_GHZ = 2.4
+VALU_CYCLES = {"b32": 2, "f64": 4, "trans64": 8}
 STRIPE_H = 16
 
 
@@ -106,6 +110,11 @@ def parse():
                     help="N > 1: nccl (RCCL over xGMI, the measured path) or gloo (host-staged rehearsal)")
     ap.add_argument("--tree", choices=["sah", "sbvh", "reference"], default=os.environ.get("RT_BENCH_TREE", "sbvh"),
                     help="device traversal hierarchy (pixels identical either way; DESIGN.md §4)")
+    ap.add_argument("--tree-record", choices=["auto", "on", "off"], default="auto",
+                    help="after the timed run, time the same run shape on other device hierarchies (the "
+                         "reference median-split tree of BASELINE config 2, mybvh.cpp:375-539, and the SAH tree) "
+                         "and report each with its upload / build seconds (tree_records); auto = on for one GPU, "
+                         "scenes below 2^20 triangles, no --adaptive")
     ap.add_argument("--opt", action="append", default=[], metavar="FIELD=VALUE",
                     help="dev A/B: an rt_upload_options field (e.g. lds_treelet=9); pixels are identical")
     ap.add_argument("--analytic", action="store_true",
@@ -148,8 +157,11 @@ def main():
     host = rtamd.HostScene.generate(a.scene, **gen)
     build_s = host.prepare()
     upload_opts = {k: (float(v) if "." in v else int(v)) for k, v in (o.split("=", 1) for o in a.opt)}
+    t_up = time.perf_counter()
     gpu = rtamd.DeviceScene(host, device=dev, analytic=a.analytic or a.scene == "spheres",
                              tree=a.tree, **upload_opts)
+    upload_wall_s = time.perf_counter() - t_up
+    dev_build_s, dev_copy_s = gpu.upload_seconds
     params = host.render_params(a.width, a.height, a.spp)
     params.stripe_height = STRIPE_H
     params.stripe_count = n
@@ -335,6 +347,17 @@ def main():
         single["natural_order"] = natural
         single["views"] = "consecutive camera-orbit views, one per launch"
 
+    # other device hierarchies over the same records (pixels and ray counts are identical for every
+    # tree, tests/test_gpu_parity.py::test_device_tree_changes_no_pixel): the same run shape, timed the
+    # same way, with each tree's upload / build seconds -- BASELINE config 2 names the reference's
+    # median-split tree (mybvh.cpp:375-539, walked by intersectBVH_device, mytracer_gpu.cu:340-424)
+    tree_records = None
+    if a.tree_record == "on" or (a.tree_record == "auto" and n == 1 and not a.adaptive
+                                 and host.triangle_count < (1 << 20)):
+        tree_records = {}
+        for tree in [t for t in ("reference", "sah", "sbvh") if t != a.tree]:
+            tree_records[tree] = tree_record(host, dev, a, upload_opts, tree, cams, F, fbufs[0], stream,
+                                             rays_of(st), timed_region)
     tot = torch.tensor([rays_timed_local, rays_frame0_local, work_bytes_frame], dtype=torch.float64, device="cuda")
     if n > 1:
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
@@ -385,7 +408,7 @@ def main():
             "valu_roof": pmc_valu_roof(workload_key(a, n), frames_per_launch, kernel_s / frames_per_launch),
         })
         out = {
-            "metric": "Mrays/sec (primary+shadow+reflect), Office 1920x1080 1spp",
+            "metric": f"Mrays/sec (primary+shadow+reflect), {workload_label(a, host.triangle_count)}",
             "value": round(mrays, 2),
             "unit": "Mrays/s",
             "n_gpus": n,
@@ -419,6 +442,11 @@ def main():
                 "adaptive_pass": adaptive_info,
                 "analytic_prims": bool(gpu.analytic),
                 "host_bvh_build_s": round(build_s, 4),
+                # rt_scene_upload: the device layout built on the host (hierarchy, wide collapse,
+                # records), then allocation + H2D copies (rt_scene_upload_seconds); excluded from value
+                "device_tree_build_s": round(dev_build_s, 4),
+                "upload_copy_s": round(dev_copy_s, 4),
+                "upload_wall_s": round(upload_wall_s, 4),
                 # frames the production kernel rendered in this process (counting launches, warm-up,
                 # timed run, single-frame run): the divisor tools/pmc_summary.py uses for per-frame bytes
                 "production_frames_rendered": (F + rem + NS + a.warmup + a.steps + (3 * NS if single else 0)
@@ -427,6 +455,7 @@ def main():
                 **({"upload_options": upload_opts} if upload_opts else {}),
             },
             "single_frame": single,
+            "tree_records": tree_records,
             "roofline": roof,
             "cpu_baseline": None,
         }
@@ -436,6 +465,63 @@ def main():
     if n > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def tree_record(host, dev, a, upload_opts, tree, cams, F, fbuf, stream, rays_launch, timed_region):
+    """Uploads the scene with device hierarchy `tree` and times a.steps frames in launches of F
+    (after min(a.warmup, F) warm-up frames), as the main run; returns Mrays/s, ms per frame and the
+    upload seconds.  Rays per launch are counted again and must equal the main tree's."""
+    t0 = time.perf_counter()
+    g = rtamd.DeviceScene(host, device=dev, analytic=a.analytic or a.scene == "spheres", tree=tree, **upload_opts)
+    wall = time.perf_counter() - t0
+    b_s, c_s = g.upload_seconds
+    outs = [fbuf[f].data_ptr() for f in range(F)]
+    stt = g.launch_frames(cams[:F], outs, stats=True, stream=stream) if F > 1 else \
+        g.launch(cams[0], outs[0], stats=True, stream=stream)
+    rays = stt.primary_rays + stt.shadow_rays + stt.reflection_rays
+    if rays != rays_launch:
+        raise RuntimeError(f"tree {tree}: {rays} rays per launch, main tree {rays_launch}")
+    ev = []
+
+    def run(frames, timed):
+        done = 0
+        while done < frames:
+            nf = min(F, frames - done)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            if nf > 1:
+                g.launch_frames(cams[:nf], outs[:nf], stats=False, stream=stream)
+            else:
+                g.launch(cams[0], outs[0], stats=False, stream=stream)
+            e1.record()
+            if timed:
+                ev.append((e0, e1, nf))
+            done += nf
+
+    n_full, rem = divmod(a.steps, F)
+    total_rays = n_full * rays_launch
+    if rem:
+        sr = g.launch_frames(cams[:rem], outs[:rem], stats=True, stream=stream) if rem > 1 else \
+            g.launch(cams[0], outs[0], stats=True, stream=stream)
+        total_rays += sr.primary_rays + sr.shadow_rays + sr.reflection_rays
+    run(min(a.warmup, F), False)
+    el = timed_region(lambda: run(a.steps, True))
+    kern = sum(e0.elapsed_time(e1) for e0, e1, _ in ev) / a.steps
+    g.close()
+    return {"value": round(total_rays / el / 1e6, 2), "unit": "Mrays/s", "ms_per_frame": round(el / a.steps * 1e3, 4),
+            "kernel_ms_per_frame": round(kern, 4), "frames_per_launch": F, "rays_identical": True,
+            "device_tree_build_s": round(b_s, 4), "upload_copy_s": round(c_s, 4), "upload_wall_s": round(wall, 4),
+            "tree": {"reference": "reference median-split tree (mybvh.cpp:375-539), oversize leaves refined, 4-wide",
+                     "sah": "binned-SAH hierarchy, 4-wide", "sbvh": "binned SAH with spatial splits, 4-wide"}[tree]}
+
+
+def workload_label(a, n_tris):
+    """The metric's workload name: BASELINE.json's own wording for the Office config ("Office
+    1920x1080 1spp"; the office_proxy stand-in), else the scene actually rendered."""
+    name = {"office": "Office", "spheres": "o_01_spheres", "cornell": "cornell"}.get(a.scene, a.scene)
+    if a.scene == "random_tris":
+        name = f"random_tris {n_tris / 1e6:g}M" if n_tris >= 1e6 else f"random_tris {n_tris}"
+    return f"{name} {a.width}x{a.height} {a.spp * a.spp}spp" + (" + adaptive pass" if a.adaptive else "")
 
 
 def default_frames(a):
@@ -518,34 +604,44 @@ def pmc_wave_mix(key, frames_per_launch=None):
             "other_frac": round(1.0 - issue - wait, 3), "source": str(path.relative_to(ROOT))}
 
 
+def valu_issue_cycles(d):
+    """SIMD cycles of VALU issue per frame from a PMC summary's instruction classes: fp64 add / mul /
+    fma at 4 cycles, fp64 transcendentals at 8, every other wave64 VALU instruction at 2
+    (VALU_CYCLES); None without the class counters."""
+    try:
+        total = d["SQ_INSTS_VALU"]["per_frame"]
+        f64 = sum(d[f"SQ_INSTS_VALU_{c}_F64"]["per_frame"] for c in ("ADD", "MUL", "FMA"))
+        trans = d["SQ_INSTS_VALU_TRANS_F64"]["per_frame"]
+    except (KeyError, TypeError):
+        return None
+    b32 = total - f64 - trans
+    return {"cycles": VALU_CYCLES["b32"] * b32 + VALU_CYCLES["f64"] * f64 + VALU_CYCLES["trans64"] * trans,
+            "insts": total, "b32": b32, "f64": f64, "trans64": trans}
+
+
 def pmc_valu_roof(key, frames_per_launch, kernel_s_per_frame):
-    """The resource that binds the render kernel: VALU issue.  achieved = wave-level
-    VALU instructions per frame (rocprofv3 SQ_INSTS_VALU of this workload, newest committed summary,
-    as pmc_per_frame picks it) / this run's kernel time per frame, against VALU_PEAK_GINSTS;
-    busy_frac = SQ_ACTIVE_INST_VALU (quad-cycles) x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs) of
-    the profiled run itself.  None when no such pass was committed."""
+    """VALU issue against the SIMDs' issue capacity: the SIMD cycles the frame's VALU
+    instructions need (valu_issue_cycles: each class at its own cost, from the newest committed
+    summary of this workload, picked as pmc_per_frame picks it) / the cycles 1024 SIMDs offer at
+    2.4 GHz in this run's kernel time per frame.  Not the binding resource (frac ~0.5 on the office):
+    each wave's dependent chain is -- see wave_cycles.  None when no such pass was committed."""
     cands = []
     for path, d in _newest_first(key):
-        try:
-            insts = d["SQ_INSTS_VALU"]["per_frame"]
-        except (KeyError, TypeError):
-            continue
-        busy = None
-        try:
-            busy = d["SQ_ACTIVE_INST_VALU"]["per_frame"] * 4 / (1024 * d["GRBM_GUI_ACTIVE"]["per_frame"] / 8)
-        except (KeyError, TypeError, ZeroDivisionError):
-            pass
-        cands.append((_profile_tag(path), path, d, insts, busy))
+        v = valu_issue_cycles(d)
+        if v is not None:
+            cands.append((_profile_tag(path), path, d, v))
     if not cands:
         return None
     same_round = [c for c in cands if c[0] == cands[0][0]]
-    _, path, d, insts, busy = next((c for c in same_round if frames_per_launch is not None
-                                    and c[2].get("_bench", {}).get("frames_per_launch") == frames_per_launch),
-                                   same_round[0])
-    achieved = insts / kernel_s_per_frame / 1e9
-    return {"unit": "G wave-instr/s", "achieved": round(achieved, 1), "peak": round(VALU_PEAK_GINSTS, 1),
-            "frac": round(achieved / VALU_PEAK_GINSTS, 4), "valu_insts_per_frame": int(insts),
-            "busy_frac": round(busy, 4) if busy is not None else None, "source": str(path.relative_to(ROOT))}
+    _, path, d, v = next((c for c in same_round if frames_per_launch is not None
+                          and c[2].get("_bench", {}).get("frames_per_launch") == frames_per_launch), same_round[0])
+    avail = VALU_SIMDS * VALU_CLOCK_GHZ * 1e9 * kernel_s_per_frame
+    return {"unit": "SIMD-cycles/frame", "achieved": int(v["cycles"]), "peak": int(avail),
+            "frac": round(v["cycles"] / avail, 4), "valu_insts_per_frame": int(v["insts"]),
+            "insts_b32": int(v["b32"]), "insts_f64": int(v["f64"]), "insts_trans_f64": int(v["trans64"]),
+            "pricing": "2 cycles per 32-bit wave64 VALU instruction per SIMD-32, 4 per fp64, 8 per fp64 "
+                       "transcendental (MI355X_MICROARCH.md cycle constants); 1024 SIMDs x 2.4 GHz",
+            "source": str(path.relative_to(ROOT))}
 
 
 def usable_cpus():

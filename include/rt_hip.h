@@ -107,8 +107,9 @@ enum {
                                   the previous one of the same image geometry (animation: frame i - 2's costs
                                   order frame i), and this launch's costs are kept; shortens the end-of-launch
                                   drain, pixels unchanged.  The DEFAULT for one-frame launches
-                                  that follow the scene's previous launch on the same stream; this flag also
-                                  orders a launch on another stream (it then waits for the previous launch).
+                                  on the stream of the scene's last ordered launch (or the first one-frame
+                                  launch); launches on another stream keep the natural order unless they set
+                                  this flag, which then makes them wait for the last ordered launch.
                                   Launches of several frames and adaptive passes keep the natural order and
                                   record nothing; one-frame launches of more than 32768 tiles (8x8 pixels) keep
                                   the natural order */
@@ -181,22 +182,28 @@ enum { RT_COLLAPSE_GREEDY = 0, RT_COLLAPSE_SAH = 1, RT_COLLAPSE_BY_SIZE = 2 };
 
 /* Upload options.  The library reads nothing from the environment: its behaviour depends only
  * on these fields and the call's arguments.  Fill with rt_upload_options_init (the defaults),
- * then change fields.  None of them changes a pixel or a ray count: they pick
- * the device hierarchy, its build, and the kernel's LDS / grid layout. */
+ * then change fields:
+ *     rt_upload_options o; rt_upload_options_init(&o); o.device_tree = RT_TREE_SAH;
+ * A zero-initialised struct is valid too: zero in sbvh_bins, sbvh_c_trav, collapse_c_tri and
+ * lds_treelet means their defaults; zero in device_tree / collapse / sbvh_alpha / sbvh_budget
+ * selects RT_TREE_SAH / RT_COLLAPSE_GREEDY / alpha 0 / budget 0 (valid, but not the defaults).
+ * None of them changes a pixel or a ray count: they pick the device hierarchy,
+ * its build, and the kernel's LDS / grid layout. */
 typedef struct rt_upload_options {
   int device_tree;       /* RT_TREE_* (default RT_TREE_SBVH) */
-  int build_threads;     /* host threads of the builders; 0 = the hardware threads, at most 64.
+  int build_threads;     /* host threads of the builders; 0 = the CPUs this process may use (its
+                            affinity mask, capped by a cgroup CPU quota), at most 64.
                             The hierarchy does not depend on it */
   int stack_ring;        /* LDS stack-ring entries of the production kernel: 0 = by size (16 from 2^18
                             device records on, else 8; default), 8 or 16 */
-  int lds_treelet;       /* 4-wide nodes each block caches in LDS: < 0 = as many as fit (default),
-                            else at most this many */
+  int lds_treelet;       /* 4-wide nodes each block caches in LDS: 0 = as many as fit (default),
+                            > 0 = at most this many, -1 = none */
   int collapse;          /* RT_COLLAPSE_* (default RT_COLLAPSE_BY_SIZE: SAH from 2^18 input triangles on,
                             else greedy) */
   int sbvh_leaf_max;     /* SBVH: SAH-terminated leaves of up to this many references, 1..8 (1 = split
                             down to single references); 0 = by size (default): 1 from 2^18 input
                             triangles on, else 2 */
-  int sbvh_bins;         /* SBVH: spatial bins per axis (default 32), 2..128 */
+  int sbvh_bins;         /* SBVH: spatial bins per axis (default 32; 0 = default), 2..128 */
   int blocks_per_cu;     /* persistent blocks per CU: 0 = as many as fit (default), else at most this many */
   int grid_spare;        /* block slots of the persistent grid left free for concurrent kernels (default 0) */
   int verbose;           /* 1: build phase times to stderr (default 0) */
@@ -205,8 +212,9 @@ typedef struct rt_upload_options {
                             0 from 2^18 input triangles on, else 1e-5 */
   double sbvh_budget;    /* SBVH: at most this many extra references per triangle; < 0 = by size
                             (default): 1.5 from 2^18 input triangles on, else 0.75 */
-  double sbvh_c_trav;    /* SBVH: node visit cost in triangle tests, for leaf termination (default 1.0) */
-  double collapse_c_tri; /* RT_COLLAPSE_SAH: cost of a leaf slot per unit area (default 1.0) */
+  double sbvh_c_trav;    /* SBVH: node visit cost in triangle tests, for leaf termination (default 1.0;
+                            0 = default) */
+  double collapse_c_tri; /* RT_COLLAPSE_SAH: cost of a leaf slot per unit area (default 1.0; 0 = default) */
   int reserved_[8];
 } rt_upload_options;
 
@@ -226,6 +234,13 @@ int rt_scene_upload_multi(const rt_scene_soa* soa, const rt_bvh_soa* bvh, const 
 
 /* Device bytes held by the scene (nodes, triangles, shading data). */
 long long rt_scene_device_bytes(const rt_scene* scene);
+
+/* Host seconds of the scene's upload: build_s = the device layout built on the host (the device
+ * hierarchy -- SBVH / SAH / refined reference tree --, its wide collapse, the triangle and shading
+ * records; once for every device of rt_scene_upload_multi), copy_s = device allocation and the
+ * H2D copies of this device.  The reference's own build (BVH::initSoA, mybvh.cpp:375-406) is the
+ * caller's rt_host_prepare, timed separately.  Either pointer may be NULL. */
+int rt_scene_upload_seconds(const rt_scene* scene, double* build_s, double* copy_s);
 
 /* Opt-in analytic primitives: the spheres and planes of the
  * raw scene (rt_raw_scene.spheres / .planes), tested in fp64 before the BVH in

@@ -38,6 +38,7 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <cfloat>
 #include <cmath>
 #include <cstdio>
@@ -59,51 +60,33 @@ using namespace rtk;
 
 namespace {
 
-#ifndef RT_BLOCK
-#define RT_BLOCK 256
-#endif
-constexpr int kBlock = RT_BLOCK;   // threads per persistent block
+constexpr int kBlock = 256;        // threads per persistent block
 constexpr int kGroups = 8;          // work heads (XCD groups)
-#ifndef RT_REFILL
-#define RT_REFILL 16
-#endif
-constexpr int kRefill = RT_REFILL;  // refill a wave when this many lanes are idle
+constexpr int kRefill = 16;         // refill a wave when this many lanes are idle (8 / 32: +-0.2 %)
 constexpr int kCtrWords = 40;       // [8,16) stats (STATS variants), [16,40) diagnostics (31: guard)
-#ifndef RT_SHORT_STACK
-#define RT_SHORT_STACK 8
-#endif
 // Traversal stack: the top kShortStack entries live in an LDS ring (slot i & kStackMask),
 // deeper entries spill to a per-lane global array.  Bounds LDS per block independently
 // of tree depth, so occupancy stays VGPR-limited.
-constexpr int kShortStack = RT_SHORT_STACK;
+constexpr int kShortStack = 8;
 // Top treelet in LDS: the first kTopNodes 4-wide nodes (breadth-first numbering) are copied
 // into each block's LDS; a node iteration whose active lanes all sit in the treelet reads
 // LDS instead of the vector-L1 path.  0 disables.
 // LDS per thread: kSlotDoubles fp64 slot words, task + visibility words, the stack ring
-#define RT_SLOT_DOUBLES 10
-#ifndef RT_TOP_NODES   // fills the CU's 160 KB at 4 blocks with the slots, ring, lights, pool
-#define RT_TOP_NODES \
-  ((40960 - RT_BLOCK * (RT_SLOT_DOUBLES * 8 + (2 + RT_SHORT_STACK) * 4) - RT_MAX_LIGHTS * 48 - 64) / 128)
-#endif
-constexpr int kTopNodes = RT_TOP_NODES > 0 ? RT_TOP_NODES : 1;
+constexpr int kSlotDoubles = 10;
+// fills the CU's 160 KB at 4 blocks with the slots, ring, lights, pool (73 nodes)
+constexpr int kTopNodes = (40960 - kBlock * (kSlotDoubles * 8 + (2 + kShortStack) * 4) - RT_MAX_LIGHTS * 48 - 64) / 128;
 constexpr int kStackMask = kShortStack - 1;
 // Tail compaction: once the work queue is empty, a wave with at most kDonateMax
 // pixels in flight hands them to the other waves of its block and exits, so the last pixels
 // of a launch run in fewer, fuller waves.  A handed-over lane's registers travel through the
 // donor thread's LDS stack entries (free between traversals): kMigWords words (packed; the
 // closest-hit distance and the hit attributes travel in the LDS slot, copied with it).
-#ifndef RT_BAND_ORDER   // several frames per launch: band-major work order
-#define RT_BAND_ORDER 1
-#endif
-#ifndef RT_DONATE_MAX
-#define RT_DONATE_MAX 24
-#endif
-constexpr int kDonateMax = RT_DONATE_MAX;
+constexpr int kDonateMax = 24;   // (0 = tail compaction off: -2.8 % batched, -1.4 % one frame)
 constexpr int kMigWords = 8;
 static_assert(kMigWords <= kShortStack, "migration words travel in the stack ring entries");
 constexpr int kPoolBytes = 64;   // LDS: live-wave count, one 64-bit lane mask per wave of the block, exhausted heads
-static_assert(8 + 8 * (RT_BLOCK / 64) + 4 <= kPoolBytes, "compaction pool does not fit");
-static_assert((kShortStack & kStackMask) == 0, "RT_SHORT_STACK must be a power of two");
+static_assert(8 + 8 * (kBlock / 64) + 4 <= kPoolBytes, "compaction pool does not fit");
+static_assert((kShortStack & kStackMask) == 0, "the stack ring must be a power of two");
 
 // Lane states.  Owners carry a pixel (CLOSEST: closest-hit ray in flight; SHADOW: a
 // batch of shadow rays in flight).  Idle lanes (FETCH / DONE) may be lent to an
@@ -135,23 +118,8 @@ typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ double buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
   return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
 }
-// measurement-only builds (make variant V=-DRT_DBG_NO_IMAGE_ST / -DRT_DBG_NO_PSTATE_ST; wrong pixels):
-// attribute the HBM write traffic (profiles/r03/write_traffic_r03.json)
-#ifdef RT_DBG_NO_IMAGE_ST
-constexpr bool kDbgNoImage = true;
-#else
-constexpr bool kDbgNoImage = false;
-#endif
-#ifdef RT_DBG_NO_PSTATE_ST
-constexpr bool kDbgNoPathState = true;
-#else
-constexpr bool kDbgNoPathState = false;
-#endif
-#ifndef RT_PS_AUX
-#define RT_PS_AUX 0   // cache-policy bits of path-state stores (dev experiments)
-#endif
 __device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, double x) {
-  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, x), r, voff, soff, RT_PS_AUX);
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, x), r, voff, soff, 0);
 }
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 struct D2 {
@@ -164,31 +132,16 @@ __device__ __forceinline__ D2 buf_ld2(__amdgpu_buffer_rsrc_t r, uint32_t voff, u
 // (no b128 store helper: path-state stores are b64, see ST4 in render_kernel)
 
 
-#ifndef RT_DPP_SCAN
-#define RT_DPP_SCAN 0   // A/B: fan-out prefix sum by DPP row shifts / broadcasts instead of __shfl_up (+-0.5 %, off)
-#endif
-// Inclusive prefix sum over the wave's 64 lanes (all lanes active): DPP row_shr 1, 2, 4, 8 within each
-// 16-lane row, then row_bcast:15 (rows 1, 3 add the last lane of the row below) and row_bcast:31 (rows
-// 2, 3 add lane 31) -- six VALU instead of six ds_bpermute round trips.  Lanes a DPP source does not
-// reach (outside the row, or rows the row mask leaves out) add the `old` operand, 0.
+// Inclusive prefix sum over the wave's 64 lanes (all lanes active).  (A DPP row-shift / broadcast scan
+// measured +-0.5 %: not kept.)
 __device__ __forceinline__ int wave_incl_scan(int x) {
-  if (!RT_DPP_SCAN) {
-    int incl = x;
+  int incl = x;
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int v = __shfl_up(incl, o);
-      if ((int)(threadIdx.x & 63) >= o) incl += v;
-    }
-    return incl;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(incl, o);
+    if ((int)(threadIdx.x & 63) >= o) incl += v;
   }
-  int v = x;
-  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);   // row_shr:1
-  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);   // row_shr:2
-  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);   // row_shr:4
-  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);   // row_shr:8
-  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);   // row_bcast:15
-  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);   // row_bcast:31
-  return v;
+  return incl;
 }
 
 // Lane of the k-th (0-based) set bit of m (k < popcount(m)).
@@ -343,9 +296,6 @@ __device__ __forceinline__ D3 normalize(D3 v) {
   if (n > 0.0) return D3{v.x / n, v.y / n, v.z / n};
   return v;
 }
-#ifndef RT_SHARED_RCP
-#define RT_SHARED_RCP 1   // A/B: normalize() with one reciprocal for its three divisions
-#endif
 // normalize: the same sqrt, then x / n for each component -- with ONE refined reciprocal of n for
 // the three divisions.  The compiler's correctly rounded fp64 division is
 //   d0 = div_scale(n), r = rcp(d0), r = fma(r, fma(-d0, r, 1), r) twice, q = d1 * r,
@@ -357,24 +307,11 @@ __device__ __forceinline__ D3 normalize(D3 v) {
 // outside it (a zero component included) normalize runs.  n = |v| is returned too (the shadow ray's
 // light distance is that same sqrt).  (Production variants only: in the diagnostic ones the extra
 // live ranges spill.)
-#ifndef RT_IDLE_LIST
-#define RT_IDLE_LIST 0   // A/B: fan-out reads helpers from a ranked idle-lane list (no kth_set_bit; +-0.5 %, off)
-#endif
-#ifndef RT_FAST_SQRT
-#define RT_FAST_SQRT 1   // A/B: sqrt of a guarded normal argument without the scaling / class fix-ups
-#endif
-#ifndef RT_AB_RCP
-#define RT_AB_RCP 1      // A/B: the barycentric quotients Da / S, Db / S with one reciprocal
-#endif
-#ifndef RT_TRI_RCP
-#define RT_TRI_RCP 0     // A/B: the triangle test's three divisions by S with one reciprocal (-0.9 %, off)
-#endif
 // sqrt of q >= 2^-767, finite: the compiler's fp64 sqrt expansion is "scale q up by 2^256 if below
 // 2^-767, v_rsq_f64 + two Newton refinements, scale back, return q itself for +-0 / +inf"; for such
 // q the scaling and the fix-up are identities, and this is the rest of it -- the same operations in
 // the same order, bit-identical to sqrt(q).
 __device__ __forceinline__ double sqrt_normal(double q) {
-  if (!RT_FAST_SQRT) return sqrt(q);
   const double y = __builtin_amdgcn_rsq(q);
   double g = q * y, h = y * 0.5;
   const double r = __builtin_fma(-h, g, 0.5);
@@ -396,11 +333,10 @@ __device__ __forceinline__ double div_by(double x, double n, double r) {
   return __builtin_fma(__builtin_fma(-n, q, x), r, q);
 }
 // |x| in [2^-300, 2^300]: quotients of two such values need neither div_scale nor div_fixup
-__device__ __forceinline__ bool div_safe(double x) { return fabs(x) >= 0x1p-300 && fabs(x) <= 0x1p300; }
 __device__ __forceinline__ D3 normalize_rcp(D3 v, double& n) {
   // every |component| >= 2^-200 and |v|^2 <= 2^400 (so every |component| <= 2^200); NaN / inf fail
   const double q = dot(v, v);
-  const bool ok = RT_SHARED_RCP && fabs(v.x) >= 0x1p-200 && fabs(v.y) >= 0x1p-200 && fabs(v.z) >= 0x1p-200 &&
+  const bool ok = fabs(v.x) >= 0x1p-200 && fabs(v.y) >= 0x1p-200 && fabs(v.z) >= 0x1p-200 &&
                   q <= 0x1p400;
   if (!ok) {
     n = sqrt(q);
@@ -410,14 +346,6 @@ __device__ __forceinline__ D3 normalize_rcp(D3 v, double& n) {
   const double r = rcp_refined(n);
   return D3{div_by(v.x, n, r), div_by(v.y, n, r), div_by(v.z, n, r)};
 }
-#ifndef RT_FAST_SHADE
-#define RT_FAST_SHADE 3   // A/B: bit 0 normalize_shade, bit 1 pow_shade
-#endif
-#ifndef RT_MED3_WINDOW
-#define RT_MED3_WINDOW 1   // A/B: the node loop's t-window bound through med3 (no per-iteration canonicalize)
-#endif
-#define RT_NORM_SHADE(v) ((RT_FAST_SHADE & 1) ? normalize_shade(v) : normalize(v))
-#define RT_POW_SHADE(x, y) ((RT_FAST_SHADE & 2) ? pow_shade(x, y) : pow(x, y))
 // Shading-only helpers for the specular term (never a ray, never a branch that switches a term on or
 // off): results within a few ulp of the reference's sqrt-and-divide normalisation and libm pow --
 // far inside the fp64 parity tolerance (1e-12), while everything that defines a ray (camera, shadow
@@ -576,10 +504,7 @@ __device__ __forceinline__ TriOps load_tri(const GTri* tris, uint32_t i) {
 // the bounce being shaded lives in the slot's aux words (below).
 //   a suspended traversal (R_SUSP, SUSP variants: cur, postponed leaf, stack pointers, hit so far).
 enum : int { R_SCOLW = 0, R_PCOL = 1, R_HD = 2, R_LACC = 3, R_SUSP = 4, kRegions = 5 };
-#ifndef RT_PS_LANE_REC
-#define RT_PS_LANE_REC 32
-#endif
-constexpr uint32_t kLaneRec = RT_PS_LANE_REC;     // bytes per lane and region
+constexpr uint32_t kLaneRec = 32;                 // bytes per lane and region
 constexpr uint32_t kRegionBytes = 64 * kLaneRec;  // 2 KB per wave and region
 
 // LDS slots ([field][thread], conflict-free): the ray (the only hand-over between the
@@ -590,7 +515,6 @@ constexpr uint32_t kRegionBytes = 64 * kLaneRec;  // 2 KB per wave and region
 //     re-loading the triangle record and recomputing the determinants (same operands, same
 //     operations: bit-identical);
 //   shadow batch in flight: the hit normal HN of the bounce being shaded.
-constexpr int kSlotDoubles = RT_SLOT_DOUBLES;
 struct RaySlots {
   double* o[3];
   double* d[3];
@@ -614,9 +538,7 @@ __device__ __forceinline__ uint32_t u4c(const uint4& v, int c) {
 }
 
 
-#ifndef RT_WAVES_PER_EU
-#define RT_WAVES_PER_EU 4   // 4 waves/SIMD = 16 waves/CU (register budget 128 VGPRs)
-#endif
+constexpr int kWavesPerEU = 4;   // 4 waves/SIMD = 16 waves/CU (register budget 128 VGPRs)
 
 // RING: entries of the per-lane traversal-stack ring in LDS (8: room for the 73-node treelet;
 // 16: deep hierarchies, e.g. millions of random triangles, which spill an 8-entry ring often;
@@ -634,11 +556,9 @@ constexpr long long kOrderMaxRange = (long long)kBlock * kOrderItems;   // tiles
 // Sort keys: a log-scale cost class (4 per octave from 2^8 ticks; 16 per octave: -1.5 %, 1 per
 // octave: +-0, profiles/r03/r03u_ab_order_*.txt) inverted so that higher costs sort first, above the
 // 12-bit local index; one radix pass over the 8 class bits (stable: equal classes keep band order).
-#ifndef RT_ORDER_SHIFT
-#define RT_ORDER_SHIFT 21   // cost classes per octave: 2^(23 - RT_ORDER_SHIFT)
-#endif
+constexpr int kOrderShift = 21;   // cost classes per octave: 2^(23 - kOrderShift)
 __device__ __forceinline__ uint32_t order_class(uint32_t cost) {
-  const int q = (int)(__float_as_uint((float)cost) >> RT_ORDER_SHIFT) - ((127 + 8) << (23 - RT_ORDER_SHIFT));
+  const int q = (int)(__float_as_uint((float)cost) >> kOrderShift) - ((127 + 8) << (23 - kOrderShift));
   return 255u - (uint32_t)min(255, max(0, q));
 }
 __device__ void order_range(const uint32_t* cost, uint32_t* order, long long n_tiles, int h, unsigned char* lds) {
@@ -666,12 +586,9 @@ __device__ void order_range(const uint32_t* cost, uint32_t* order, long long n_t
 // idle ones and resumes the parked rays beside the new ones.  Raises SIMD efficiency where rays of a
 // wave differ widely in length (incoherent scenes); no fan-out in these variants.
 constexpr int kSuspBit = 8;
-#ifndef RT_SUSP_ACTIVE
-#define RT_SUSP_ACTIVE 16
-#endif
-constexpr int kSuspActive = RT_SUSP_ACTIVE;   // 16 (config 4: 8 +2.8 %, 16 +3.2 %, 32 +1.8 %, 48 -8 %)
+constexpr int kSuspActive = 16;   // 16 (config 4: 8 +2.8 %, 16 +3.2 %, 32 +1.8 %, 48 -8 %)
 template <int WIDTH, bool STATS, bool TL = false, int RING = kShortStack, bool SUSP = false>
-__global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render_kernel(KParams P) {
+__global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_kernel(KParams P) {
   static_assert(RING >= kMigWords && (RING & (RING - 1)) == 0, "ring: a power of two holding the migration words");
   constexpr int kRingMask = RING - 1;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
@@ -745,7 +662,6 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
     w = b.b;
   };
   auto ST4 = [&](int r, D3 v, double w) {
-    if (kDbgNoPathState) return;   // measurement-only build (wrong pixels): HBM writes without path state
     const uint32_t o = (uint32_t)r * kRegionBytes;
     buf_st(prs, pvo, o, v.x); buf_st(prs, pvo, o + 8u, v.y); buf_st(prs, pvo, o + 16u, v.z); buf_st(prs, pvo, o + 24u, w);
   };
@@ -852,7 +768,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
   auto start_sample = [&]() {
     const int n = P.spp_n;
     double X, Y;
-    if (RT_SHARED_RCP && n == 1) {   // xo = 0/1 - 0.5 + 1/2 = +0 exactly: X = px + 0 = px
+    if (n == 1) {   // xo = 0/1 - 0.5 + 1/2 = +0 exactly: X = px + 0 = px
       X = (double)px;
       Y = (double)py;
     } else {
@@ -916,7 +832,6 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
             lrow = id != 0xffffffffu ? (int)(pix / (uint32_t)P.W) : P.rows;
             item = wk;
           } else {
-#if RT_BAND_ORDER
             // (tile indices < 2^31, checked at launch: 32-bit divisions by the launch's invariant
             // divisors as a multiply-high and a shift, DivMagic)
             const uint32_t tile = P.tile_order ? P.tile_order[wk >> 6] : (uint32_t)(wk >> 6);
@@ -928,14 +843,6 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
             const uint32_t rem = tile - ty * row_tiles;
             frame = P.n_frames > 1 ? (int)P.div_tiles_x.div(rem) : 0;
             const int tx = (int)(rem - (uint32_t)frame * (uint32_t)P.tiles_x);
-#else
-            long long tile = wk >> 6;
-            const int j = (int)(wk & 63);
-            frame = P.n_frames > 1 ? (int)(tile / P.frame_tiles) : 0;
-            tile -= (long long)frame * P.frame_tiles;
-            const long long ty = tile / P.tiles_x;
-            const int tx = (int)(tile - ty * P.tiles_x);
-#endif
             px = tx * 8 + (j & 7);
             lrow = (int)ty * 8 + (j >> 3);
           }
@@ -1079,7 +986,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
         for (int k = 0; k < 3; ++k) {
           float df = (float)d3v[k];
           if (fabsf(df) < 1e-20f) df = signbit(d3v[k]) ? -1e-20f : 1e-20f;
-          if constexpr (WIDTH == 4 && RT_SHARED_RCP) {
+          if constexpr (WIDTH == 4) {
             // v_rcp_f32 (1 ulp) + one Newton step: within about half an ulp of 1 / df, as the
             // correctly rounded division (11 VALU) it replaces; the box error bound of DESIGN.md
             // §4 stays far inside delta.  (The 2-wide canonical kernel keeps the oracle's division.)
@@ -1204,33 +1111,21 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
                                (Da + Db - S) * sS > 0x1p-40 * (fabs(Da) + fabs(Db) + aS);
               if (!out) {
                 const double Dt = det3(T.e1, T.e2, c4);
-                // the three quotients by S with one reciprocal where that is bit-identical (div_safe)
-                const bool fdiv = RT_TRI_RCP && !STATS && !TL && div_safe(S) && div_safe(Dt) && div_safe(Da) &&
-                                  div_safe(Db);
-                double rS = 0.0, t;
-                if (fdiv) {
-                  rS = rcp_refined(S);
-                  t = div_by(Dt, S, rS);
-                } else {
-                  t = Dt / S;
-                }
+                // (t's division shared with alpha / beta's reciprocal: -0.9 %, more live registers)
+                const double t = Dt / S;
                 const bool cand = anyhit ? (t < tlim) : (t <= tlim);
                 if (t > 1e-5 && cand) {
                   double alpha, beta;
                   // alpha, beta: one reciprocal of S for the two quotients where that is bit-identical:
                   // |S| >= 1e-10 here and |Da|, |Db| <= |S|(1 + 2^-48) (the early rejections), so with
                   // |Da|, |Db| >= |S| 2^-900 and |S| < 2^1000 no operand or quotient is denormal, zero or
-                  // near an exponent limit (RT_AB_RCP; RT_TRI_RCP shares t's division as well)
+                  // near an exponent limit
                   const double lim = aS * 0x1p-900;
-                  const bool fab = RT_AB_RCP && !STATS && !TL && !fdiv && fabs(Da) >= lim && fabs(Db) >= lim &&
-                                   aS < 0x1p1000;
+                  const bool fab = !STATS && !TL && fabs(Da) >= lim && fabs(Db) >= lim && aS < 0x1p1000;
                   if (fab) {
                     const double r = rcp_refined(S);
                     alpha = div_by(Da, S, r);
                     beta = div_by(Db, S, r);
-                  } else if (fdiv) {
-                    alpha = div_by(Da, S, rS);
-                    beta = div_by(Db, S, rS);
                   } else {
                     alpha = Da / S;
                     beta = Db / S;
@@ -1382,13 +1277,8 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
             // the window bound enters through med3 (med3(t, lo, +inf) = max, med3(t, hi, -inf) = min;
             // no operand is ever NaN: |inv| <= 1e20, finite or empty-box planes): fminf / fmaxf of
             // the loop-carried bound made the compiler re-canonicalise it every iteration (2 VALU)
-#if RT_MED3_WINDOW
             const float tn = fmaxf(fmaxf(tx0, ty0), __builtin_amdgcn_fmed3f(tz0, lo_c, pinf));
             const float tf = fminf(fminf(tx1, ty1), __builtin_amdgcn_fmed3f(tz1, hi_c, -pinf));
-#else
-            const float tn = fmaxf(fmaxf(tx0, ty0), fmaxf(tz0, lo_c));
-            const float tf = fminf(fminf(tx1, ty1), fminf(tz1, hi_c));
-#endif
             const uint32_t r = u4c(rf, c);
             const bool h = tn <= tf;   // absent children carry the empty box [+inf, -inf]
             k[c] = h ? tn : INFINITY;
@@ -1619,11 +1509,11 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
         double refl = 0.0;
         if (diff > 0.0) {   // reflection(), mytracer.cpp:524-534
           const double s2 = 2.0 * dot(hn_, l);
-          const D3 r = RT_NORM_SHADE(sub(scl(s2, hn_), l));   // feeds only max(0, r.v)^shininess: continuous
+          const D3 r = normalize_shade(sub(scl(s2, hn_), l));   // feeds only max(0, r.v)^shininess: continuous
           refl = stdmax(0.0, dot(r, hv_));
         }
         // pow(+0, y > 0) = +0 exactly: skip the fp64 pow for the (frequent) zero highlight
-        if (!(refl == 0.0 && M.shininess > 0.0)) refl = RT_POW_SHADE(refl, M.shininess);
+        if (!(refl == 0.0 && M.shininess > 0.0)) refl = pow_shade(refl, M.shininess);
         return d3(L6.col.x * (hd_.x * diff + M.ks[0] * refl), L6.col.y * (hd_.y * diff + M.ks[1] * refl),
                   L6.col.z * (hd_.z * diff + M.ks[2] * refl));
       };
@@ -1827,7 +1717,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
           asm volatile("" : "+s"(n2));   // converted here, not hoisted into a VGPR live across the loop
           const double nn = (double)n2;
           double r, g, b;
-          if (RT_SHARED_RCP && (n2 & (n2 - 1)) == 0) {
+          if ((n2 & (n2 - 1)) == 0) {
             // n2 = 2^k: x / n2 = x * 2^-k exactly (one rounding of the same exact value), no division
             const double s = __builtin_ldexp(1.0, -__builtin_ctz((unsigned)n2));
             r = stdmin(pcol.x * s, 1.0); g = stdmin(pcol.y * s, 1.0); b = stdmin(pcol.z * s, 1.0);
@@ -1838,8 +1728,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
           // nontemporal (evict-first): the frame is written once and never read here, so its lines
           // should not push the path-state lines out of L2 (office: HBM writes 50.9 -> 45.5 MB per
           // frame, time unchanged; profiles/r03/write_traffic_r03.json)
-          if (kDbgNoImage) {   // measurement-only build: HBM writes without the frame
-          } else if (P.out_fmt == RT_OUT_RGB_F64) {
+          if (P.out_fmt == RT_OUT_RGB_F64) {
             double* out = reinterpret_cast<double*>(P.frames[frame].out) + o;
             __builtin_nontemporal_store(r, out); __builtin_nontemporal_store(g, out + 1);
             __builtin_nontemporal_store(b, out + 2);
@@ -1860,12 +1749,6 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
       const unsigned long long I = wballot(idle);
       if (I != 0ull && wballot(want > 0) != 0ull) {
         if (idle) ltask[threadIdx.x] = kTaskNone;
-#if RT_IDLE_LIST
-        // the idle lanes by rank, in entry 0 of the wave's stack-ring row (free between traversals:
-        // tail compaction's words were read before SHADE, and the SUSP variants, which park stacks in
-        // the ring, lend no lanes): an owner's t-th helper is one LDS read instead of a bit search
-        if (idle) reinterpret_cast<uint32_t*>(lds_raw)[wbase + __popcll(I & lane_below)] = (uint32_t)lane;
-#endif
         const int incl = wave_incl_scan(want);   // inclusive prefix sum of want over the wave
         wave_lds_sync();
         const int off = incl - want;
@@ -1874,11 +1757,7 @@ __global__ void __launch_bounds__(kBlock, RT_WAVES_PER_EU * 256 / kBlock) render
         if (got > 0) {
           const int n_extra_lights = min(P.n_lights - light - 1, kBatchExtra);
           for (int t = 0; t < got; ++t) {   // task words only: each helper derives its own ray
-#if RT_IDLE_LIST
-            const int ht = wbase + (int)reinterpret_cast<const uint32_t*>(lds_raw)[wbase + off + t];
-#else
-            const int ht = wbase + kth_set_bit(I, off + t);
-#endif
+            const int ht = wbase + kth_set_bit(I, off + t);   // (a ranked idle-lane list instead: +-0.5 %)
             uint32_t tw;
             if (t < n_extra_lights) {
               tw = (uint32_t)lane | ((uint32_t)(t + 1) << 6) | ((uint32_t)(light + 1 + t) << 11);
@@ -2016,10 +1895,7 @@ struct ShardRows {
 // device atomic (one per wave serialised ~8 k atomics on the counter's line: 68 us per 1080p
 // frame).
 constexpr int kSelThreads = 1024;
-#ifndef RT_SEL_TILES
-#define RT_SEL_TILES 8
-#endif
-constexpr int kSelTilesPerWave = RT_SEL_TILES;
+constexpr int kSelTilesPerWave = 8;
 constexpr int kSelTilesPerBlock = (kSelThreads / 64) * kSelTilesPerWave;
 __global__ void __launch_bounds__(kSelThreads) adaptive_select_kernel(const double* prim, const double* halo, void* out,
                                                                       int out_fmt, ShardRows G, double threshold,
@@ -2151,7 +2027,8 @@ struct Variant {
 // [0] production (4-wide), [1] 4-wide + counters, [2] canonical 2-wide counters
 // (the traversal the oracle replicates: tests pin its node / triangle counts),
 // [3] production + per-round timeline (RT_FLAG_TIMELINE, diagnostics), [4] production with a
-// 16-entry stack ring (deep hierarchies).
+// 16-entry stack ring (deep hierarchies), [5] the same with suspend/resume traversal (deep
+// hierarchies' several-frame launches).
 const Variant kVariants[] = {
     {render_kernel<4, false>, false},
     {render_kernel<4, true>, true},
@@ -2159,14 +2036,10 @@ const Variant kVariants[] = {
     {render_kernel<4, false, true>, false},
     {render_kernel<4, false, false, 16>, false},
     {render_kernel<4, false, false, 16, true>, false},
-    {render_kernel<4, false, false, 8, true>, false},
 };
-constexpr int kNumVariants = 7;
+constexpr int kNumVariants = 6;
 constexpr int kRingDeep = 16;
 inline int variant_ring(int v) { return (v == 4 || v == 5) ? kRingDeep : kShortStack; }
-#ifndef RT_SUSP_MODE
-#define RT_SUSP_MODE 1   // suspend/resume: 0 never, 1 several-frame launches of deep scenes, 2 all launches (A/B)
-#endif
 // LDS per block: the variant's stack ring (ring entries per thread, at address 0: the kernel's
 // slot offsets are compile-time constants), kSlotDoubles doubles of slot, task + visibility words.
 size_t lds_bytes(int /*stack_words*/, int ring = kShortStack) {
@@ -2258,6 +2131,13 @@ struct rt_scene {
   int last_order_buf = 0;
   uint32_t* d_tile_order = nullptr;  // rt_debug_set_tile_order: work order of launches with that many tiles
   long long tile_order_n = 0;
+  // the last launch that read or wrote the cost / order maps (ordered or cost-debug): its stream and
+  // an event recorded after it.  A map-touching launch on another stream waits for that event; an
+  // implicitly ordered launch needs that stream (stream order is then the fence)
+  bool maps_used = false;
+  hipStream_t maps_stream = nullptr;
+  hipEvent_t maps_ev = nullptr;
+  double build_s = 0.0, copy_s = 0.0;   // rt_scene_upload_seconds
 };
 
 namespace {
@@ -2339,8 +2219,9 @@ int upload_image(const SceneImage& I, const rt_upload_options& opt, int device, 
   if (opt.stack_ring != 0) sc->deep = opt.stack_ring >= 16;   // forced ring size
   for (int v = 0; v < kNumVariants; ++v) {
     int& nt = sc->n_top_v[v];
-    nt = RT_TOP_NODES > 0 ? top_nodes_for(sc->stack_words, variant_ring(v), sc->n_gnodes4) : 0;
-    if (opt.lds_treelet >= 0) nt = std::min(nt, opt.lds_treelet);   // cache fewer nodes (0 = none)
+    nt = top_nodes_for(sc->stack_words, variant_ring(v), sc->n_gnodes4);
+    if (opt.lds_treelet > 0) nt = std::min(nt, opt.lds_treelet);   // cache at most this many nodes
+    if (opt.lds_treelet < 0) nt = 0;                                // none
   }
   sc->bpc_cap = opt.blocks_per_cu;
   sc->grid_spare = opt.grid_spare;
@@ -2405,6 +2286,14 @@ int resolve_options(const rt_upload_options* opt, rt_upload_options& o) {
   upload_options_defaults(&o);
   if (!opt) return RT_OK;
   o = *opt;
+  // zero-initialised fields mean their defaults (a C caller's `rt_upload_options o = {0}` or
+  // designated initialiser stays valid and changes nothing but the fields it names)
+  rt_upload_options d;
+  upload_options_defaults(&d);
+  if (o.sbvh_bins == 0) o.sbvh_bins = d.sbvh_bins;
+  if (o.sbvh_c_trav == 0.0) o.sbvh_c_trav = d.sbvh_c_trav;
+  if (o.collapse_c_tri == 0.0) o.collapse_c_tri = d.collapse_c_tri;
+  if (o.lds_treelet < -1) return fail(RT_ERR_INVALID, "rt_scene_upload: lds_treelet must be >= -1");
   if (o.stack_ring != 0 && o.stack_ring != 8 && o.stack_ring != 16)
     return fail(RT_ERR_INVALID, "rt_scene_upload: stack_ring must be 0, 8 or 16");
   if (o.blocks_per_cu < 0 || o.grid_spare < 0 || o.build_threads < 0)
@@ -2431,9 +2320,16 @@ int rt_scene_upload_ex(const rt_scene_soa* s, const rt_bvh_soa* b, int device, c
   int rc = resolve_options(opt, o);
   if (rc != RT_OK) return rc;
   SceneImage I;
+  const auto t0 = std::chrono::steady_clock::now();
   rc = build_image(s, b, o, kTopNodes, I);
   if (rc != RT_OK) return fail(rc, build_image_error());
-  return upload_image(I, o, device, out);
+  const auto t1 = std::chrono::steady_clock::now();
+  rc = upload_image(I, o, device, out);
+  if (rc == RT_OK) {
+    (*out)->build_s = std::chrono::duration<double>(t1 - t0).count();
+    (*out)->copy_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
+  }
+  return rc;
 }
 
 int rt_scene_upload_multi(const rt_scene_soa* s, const rt_bvh_soa* b, const int* devices, int n_devices,
@@ -2444,16 +2340,24 @@ int rt_scene_upload_multi(const rt_scene_soa* s, const rt_bvh_soa* b, const int*
   int rc = resolve_options(opt, o);
   if (rc != RT_OK) return rc;
   SceneImage I;
+  const auto t0 = std::chrono::steady_clock::now();
   rc = build_image(s, b, o, kTopNodes, I);
   if (rc != RT_OK) return fail(rc, build_image_error());
+  const double build_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   // one host thread per device: the copies and context allocations proceed in parallel
   std::vector<int> rcs(n_devices, RT_OK);
   std::vector<std::string> errs(n_devices);
   std::vector<std::thread> th;
   for (int g = 0; g < n_devices; ++g)
     th.emplace_back([&, g]() {
+      const auto t1 = std::chrono::steady_clock::now();
       rcs[g] = upload_image(I, o, devices[g], &outs[g]);
-      if (rcs[g] != RT_OK) errs[g] = g_error;   // thread-local message of that thread
+      if (rcs[g] != RT_OK) {
+        errs[g] = g_error;   // thread-local message of that thread
+      } else {
+        outs[g]->build_s = build_s;
+        outs[g]->copy_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
+      }
     });
   for (auto& t : th) t.join();
   for (int g = 0; g < n_devices; ++g)
@@ -2468,6 +2372,13 @@ int rt_scene_upload_multi(const rt_scene_soa* s, const rt_bvh_soa* b, const int*
 }
 
 long long rt_scene_device_bytes(const rt_scene* s) { return s ? s->bytes : 0; }
+
+int rt_scene_upload_seconds(const rt_scene* s, double* build_s, double* copy_s) {
+  if (!s) return fail(RT_ERR_INVALID, "rt_scene_upload_seconds: null scene");
+  if (build_s) *build_s = s->build_s;
+  if (copy_s) *copy_s = s->copy_s;
+  return RT_OK;
+}
 
 int rt_rows_in_shard(const rt_render_params* p) {
   if (!p) return 0;
@@ -2614,10 +2525,13 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   // also orders launches on other streams (each then waits for the previous launch's end).
   // Diagnostics, a debug order and RT_FLAG_NATURAL_ORDER keep the natural order.
   const bool debug_order = sc->d_tile_order && sc->tile_order_n == P.n_tiles;
+  // (implicit: only on the stream of the last launch that touched the maps, so stream order fences
+  // it against that launch's reads and its drain's writes of the maps -- whatever ran on other
+  // streams in between)
   const bool implicit_order =
       !(p->flags & (RT_FLAG_TRAVERSAL_STATS | RT_FLAG_WIDE_STATS | RT_FLAG_TIMELINE | RT_FLAG_TILE_COST |
                     RT_FLAG_TILE_COST_TIME | RT_FLAG_NATURAL_ORDER)) &&
-      !debug_order && (sc->last_ctx < 0 || sc->last_stream == st);
+      !debug_order && (!sc->maps_used || sc->maps_stream == st);
   const bool cost_order = !list && n_frames == 1 && ((p->flags & RT_FLAG_COST_ORDER) || implicit_order);
   const bool cost_debug = !list && (p->flags & (RT_FLAG_TILE_COST | RT_FLAG_TILE_COST_TIME));
   if (cost_order || cost_debug) {
@@ -2639,8 +2553,8 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
     }
     sc->cost_n = n_pos;
     sc->cost_tiles_x = P.tiles_x;
-    if (sc->last_ctx >= 0 && sc->last_stream != st)   // the previous launch (another stream) is done with the maps
-      HIP_TRY(hipStreamWaitEvent(st, sc->ctx[sc->last_ctx].ev1, 0));
+    if (sc->maps_used && sc->maps_stream != st)   // the last map launch (another stream) is done with the maps
+      HIP_TRY(hipStreamWaitEvent(st, sc->maps_ev, 0));
     // cost unit: pixel lifetime (RT_FLAG_TILE_COST_TIME, and RT_FLAG_COST_ORDER alone) or bounces
     // (RT_FLAG_TILE_COST, also with RT_FLAG_COST_ORDER)
     P.cost_time = (p->flags & RT_FLAG_TILE_COST) ? 0 : 1;
@@ -2678,8 +2592,8 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
                 : (p->flags & RT_FLAG_TIMELINE) ? 3
                 // 4/5: the 16-entry-ring production variants; suspend/resume on deep scenes' several-
                 // frame launches (config 4, 128 frames: +3.2 %; one frame: -6 %, so not there)
-                : sc->deep ? ((RT_SUSP_MODE >= 2 || (RT_SUSP_MODE == 1 && n_frames > 1 && !list)) ? 5 : 4)
-                : (RT_SUSP_MODE >= 2 ? 6 : 0);
+                : sc->deep ? ((n_frames > 1 && !list) ? 5 : 4)
+                : 0;
   const int ring = variant_ring(v);
   const int n_top = sc->n_top_v[v];
   const size_t lds = lds_bytes_total(sc->stack_words, n_top, ring);
@@ -2728,6 +2642,12 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
                             args, lds, st));
   }
   HIP_TRY(hipEventRecord(C.ev1, st));
+  if (cost_order || cost_debug) {   // this launch read / wrote the maps: the next map launch is fenced on it
+    if (!sc->maps_ev) HIP_TRY(hipEventCreateWithFlags(&sc->maps_ev, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(sc->maps_ev, st));
+    sc->maps_used = true;
+    sc->maps_stream = st;
+  }
   C.used = true;
   C.variant = v;
   C.waves = rows > 0 ? blocks * (kBlock / 64) : 0;
@@ -3015,8 +2935,15 @@ int rt_debug_set_tile_order(rt_scene* sc, const unsigned int* order, long long n
   if (!sc || n < 0 || (n > 0 && !order)) return fail(RT_ERR_INVALID, "rt_debug_set_tile_order: bad argument");
   if (hipSetDevice(sc->device) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
     return fail(RT_ERR_HIP, "rt_debug_set_tile_order: synchronize failed");
-  for (long long i = 0; i < n; ++i)
-    if ((long long)order[i] >= n) return fail(RT_ERR_INVALID, "rt_debug_set_tile_order: not a permutation");
+  {   // a permutation: every index below n exactly once (a duplicate would render a tile twice and
+      // leave another unwritten)
+    std::vector<bool> seen((size_t)n, false);
+    for (long long i = 0; i < n; ++i) {
+      if ((long long)order[i] >= n || seen[order[i]])
+        return fail(RT_ERR_INVALID, "rt_debug_set_tile_order: not a permutation");
+      seen[order[i]] = true;
+    }
+  }
   if (sc->d_tile_order) (void)hipFree(sc->d_tile_order);
   sc->d_tile_order = nullptr;
   sc->tile_order_n = 0;
@@ -3139,6 +3066,7 @@ void rt_scene_free(rt_scene* sc) {
     if (c.ev0) (void)hipEventDestroy(c.ev0);
     if (c.ev1) (void)hipEventDestroy(c.ev1);
   }
+  if (sc->maps_ev) (void)hipEventDestroy(sc->maps_ev);
   delete sc;
 }
 

@@ -20,7 +20,9 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <deque>
+#include <sched.h>
 #include <string>
 #include <thread>
 #include <vector>
@@ -153,6 +155,25 @@ void build_device_tree(const rt_scene_soa* s, const rt_bvh_soa* b, DevTree& E, s
 // arenas and appended in job order, so the tree does not depend on the thread count.
 thread_local int g_threads = 1;   // build threads of the current build_image call (from the options)
 int sah_threads() { return g_threads; }
+
+// CPUs this process may run on: its affinity mask, capped by a cgroup v2 CPU quota (cpu.max
+// "quota period"); a GPU box's job sees the whole node in hardware_concurrency() but may use
+// only its share (16 CPUs per GPU there).
+int usable_cpus() {
+  int n = (int)std::thread::hardware_concurrency();
+  cpu_set_t set;
+  if (sched_getaffinity(0, sizeof set, &set) == 0) n = CPU_COUNT(&set);
+  if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char q[32] = {0};
+    long long per = 0;
+    if (std::fscanf(f, "%31s %lld", q, &per) == 2 && std::strcmp(q, "max") != 0 && per > 0) {
+      const long long quota = std::atoll(q);
+      if (quota > 0) n = std::min<long long>(n, std::max(1LL, quota / per));
+    }
+    std::fclose(f);
+  }
+  return std::max(1, n);
+}
 thread_local bool g_verbose = false;
 
 struct SahData {
@@ -895,8 +916,7 @@ int build_image(const rt_scene_soa* s, const rt_bvh_soa* b, const rt_upload_opti
   if (opt.collapse != RT_COLLAPSE_GREEDY && opt.collapse != RT_COLLAPSE_SAH)
     return fail(RT_ERR_INVALID, "rt_scene_upload: unknown collapse");
   if (opt.build_threads < 0) return fail(RT_ERR_INVALID, "rt_scene_upload: build_threads < 0");
-  g_threads = opt.build_threads > 0 ? std::min(opt.build_threads, 64)
-                                    : std::max(1, std::min((int)std::thread::hardware_concurrency(), 64));
+  g_threads = opt.build_threads > 0 ? std::min(opt.build_threads, 64) : std::max(1, std::min(usable_cpus(), 64));
   g_verbose = opt.verbose != 0;
   const bool timing = g_verbose;   // phase times to stderr (diagnostics)
   auto t_last = std::chrono::steady_clock::now();
@@ -1238,7 +1258,7 @@ void upload_options_defaults(rt_upload_options* o) {
   o->device_tree = RT_TREE_SBVH;
   o->build_threads = 0;
   o->stack_ring = 0;
-  o->lds_treelet = -1;
+  o->lds_treelet = 0;   // as many as fit
   o->collapse = RT_COLLAPSE_BY_SIZE;
   o->sbvh_leaf_max = kSbvhLeafMax;
   o->sbvh_bins = kSbvhBins;

@@ -19,6 +19,7 @@
 #include <stdexcept>
 #include <thread>
 #include <cstdlib>
+#include <sched.h>
 
 namespace rt {
 
@@ -320,7 +321,10 @@ int build_threads() {
     const char* o = std::getenv("OMP_NUM_THREADS");
     t = o ? std::atoi(o) : 0;
   }
-  if (t <= 0) t = (int)std::thread::hardware_concurrency();
+  if (t <= 0) {   // the CPUs this process may run on (affinity mask), not the whole node
+    cpu_set_t set;
+    t = sched_getaffinity(0, sizeof set, &set) == 0 ? CPU_COUNT(&set) : (int)std::thread::hardware_concurrency();
+  }
   return std::max(1, std::min(t, 64));
 }
 

@@ -239,7 +239,7 @@ class DeviceScene:
         path (mytracer_gpu.cu:314-328).  tree: None (library default, "sbvh": SAH with
         spatial splits), "sbvh", "sah" (object splits only) or "reference" -- the device
         traversal hierarchy (pixels and ray counts do not depend on it).  options: other
-        rt_upload_options fields (stack_ring=16, lds_treelet=0, sbvh_leaf_max=1, ...)."""
+        rt_upload_options fields (stack_ring=16, lds_treelet=-1 (none), sbvh_leaf_max=1, ...)."""
         self._h = C.c_void_p()
         self.device = device
         opt = upload_options(tree, **options)
@@ -271,6 +271,14 @@ class DeviceScene:
     @property
     def device_bytes(self):
         return int(hip_lib().rt_scene_device_bytes(self._h))
+
+    @property
+    def upload_seconds(self):
+        """(build_s, copy_s) of rt_scene_upload: the device layout built on the host (hierarchy,
+        collapse, records), then device allocation + H2D copies (rt_scene_upload_seconds)."""
+        b, c = C.c_double(), C.c_double()
+        _check_hip(hip_lib().rt_scene_upload_seconds(self._h, C.byref(b), C.byref(c)), "rt_scene_upload_seconds")
+        return b.value, c.value
 
     def launch(self, params, d_out, stats=False, stream=None):
         """Asynchronous render into a device buffer (int pointer); returns Stats if stats=True."""

@@ -159,6 +159,7 @@ HIP_SYMBOLS = {
                                         C.POINTER(UploadOptions), C.POINTER(C.c_void_p)]),
     "rt_scene_set_analytic": (C.c_int, [C.c_void_p, C.POINTER(Sphere), C.c_int, C.POINTER(Plane), C.c_int]),
     "rt_scene_device_bytes": (C.c_longlong, [C.c_void_p]),
+    "rt_scene_upload_seconds": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "rt_rows_in_shard": (C.c_int, [C.POINTER(RenderParams)]),
     "rt_launch_compute_image": (C.c_int, [C.c_void_p, C.POINTER(RenderParams), C.c_void_p,
                                           C.POINTER(Stats), C.c_void_p]),

@@ -57,3 +57,53 @@ def mini(name):
     meshes, lights, cam_def, bg, amb, depth = scenes()[name]
     eye, center, up, fovy, w, h = cam_def
     return minirt.Scene(meshes, lights, minirt.camera(eye, center, up, fovy, w, h), bg, amb, depth)
+
+
+# ---- inputs where the reference CPU renderer and a brute-force renderer differ ----
+# The reference's fp64 slab test (BVH::intersectAABB, mybvh.cpp:99-135) is not conservative, so a
+# ray that meets a triangle exactly on the boundary of its leaf box can lose the hit that the
+# triangle test (Mesh::intersect_triangle, mymesh.cpp:190-215, inclusive barycentrics) accepts.  The
+# kernel's boxes are conservative (outward-rounded fp32, grown by delta), so it keeps the hit, as
+# tests/minirt.py (no boxes at all) does.  Each case lists exactly the (row, col) pixels where the
+# reference differs; everywhere else all three agree.
+AXIS_CAM = ((0.0, 0.0, 4.0), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 50.0, 64, 48)
+AXIS_LIGHTS = [((0.0, 2.5, 0.0), (0.7, 0.7, 0.7)), ((0.0, 0.0, 3.0), (0.3, 0.3, 0.3))]
+
+
+def divergence_scenes():
+    """name -> (meshes, lights, cam_def, background, ambience, max_depth, spp_n,
+    expected divergent pixels [(row, col)], expected (shadow, reflection) ray-count difference
+    minirt - reference)."""
+    floor_v = [(-3.0, -1.0, 3.0), (3.0, -1.0, 3.0), (3.0, -1.0, -3.0), (-3.0, -1.0, -3.0)]   # y = -1
+    floor_t = [(0, 1, 2), (0, 2, 3)]
+    wall_v, wall_t = quad(-3.0, 3.0, -1.0, 3.0, -2.0)
+    box_v = [(-0.5, -1.0, 0.0), (0.5, -1.0, 0.0), (0.5, 0.1, 0.0), (-0.5, 0.1, 0.0)]
+    out = {}
+    # 1. edge-exact hit: at round extents one 2x2-spp sample ray of the 64x48 image meets the floor
+    #    exactly on its edge x = -3 (a face of the floor's leaf box); the reference's slabs round the
+    #    box out by an ulp and reject it, the triangle test accepts the edge point
+    out["edge_exact"] = ([minirt.Mesh(floor_v, floor_t, "FLAT", FLAT_MAT),
+                          minirt.Mesh(wall_v, wall_t, "FLAT", MIRROR_MAT),
+                          minirt.Mesh(box_v, [(0, 1, 2), (0, 2, 3)], "FLAT", FLAT_MAT)],
+                         AXIS_LIGHTS, AXIS_CAM, (0.05, 0.1, 0.2), (0.2, 0.2, 0.2), 3, 2, [(14, 3)], (2, 0))
+    # 2. NaN max plane: a panel x in [-1, 0] alone; the centre column's primary rays have d.x == 0
+    #    exactly and o.x == 0 == the leaf box's max x, where the reference's slab computes
+    #    (0 - 0) / 0 = NaN and std::min carries it into tmax (the min-plane side keeps it out):
+    #    the box is rejected, the panel's edge x = 0 is missed
+    pan_v, pan_t = quad(-1.0, 0.0, -0.5, 0.5, 1.0)
+    out["nan_max_plane"] = ([minirt.Mesh(pan_v, pan_t, "FLAT", FLAT_MAT)], AXIS_LIGHTS, AXIS_CAM,
+                            (0.05, 0.1, 0.2), (0.2, 0.2, 0.2), 3, 1, [(r, 32) for r in range(16, 33)], (34, 0))
+    return out
+
+
+def write_divergence(tmpdir, name):
+    meshes, lights, cam_def, bg, amb, depth = divergence_scenes()[name][:6]
+    path = tmpdir / f"{name}.sce"
+    minirt.write_sce(path, meshes, lights, cam_def, bg, amb, depth)
+    return path
+
+
+def mini_divergence(name):
+    meshes, lights, cam_def, bg, amb, depth = divergence_scenes()[name][:6]
+    eye, center, up, fovy, w, h = cam_def
+    return minirt.Scene(meshes, lights, minirt.camera(eye, center, up, fovy, w, h), bg, amb, depth)

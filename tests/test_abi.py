@@ -79,14 +79,15 @@ def test_upload_options_defaults_and_validation():
     # The library reads no environment: every build / layout choice is an rt_upload_options field.
     o = abi.UploadOptions()
     rtamd.hip_lib().rt_upload_options_init(C.byref(o))
-    assert (o.device_tree, o.stack_ring, o.lds_treelet, o.collapse) == (abi.RT_TREE_SBVH, 0, -1, abi.RT_COLLAPSE_BY_SIZE)
+    assert (o.device_tree, o.stack_ring, o.lds_treelet, o.collapse) == (abi.RT_TREE_SBVH, 0, 0, abi.RT_COLLAPSE_BY_SIZE)
     assert (o.sbvh_leaf_max, o.sbvh_bins, o.blocks_per_cu, o.grid_spare, o.verbose) == (0, 32, 0, 0, 0)
     assert (o.sbvh_alpha, o.sbvh_budget, o.sbvh_c_trav, o.collapse_c_tri) == (-1.0, -1.0, 1.0, 1.0)
     hs = rtamd.HostScene.generate("cornell")
     hs.prepare()
     lib = rtamd.hip_lib()
     for field, bad in (("stack_ring", 12), ("blocks_per_cu", -1), ("sbvh_bins", 1), ("sbvh_leaf_max", 9), ("sbvh_leaf_max", -1),
-                       ("device_tree", 7), ("collapse", 3), ("sbvh_alpha", float("nan")), ("sbvh_budget", float("nan"))):
+                       ("device_tree", 7), ("collapse", 3), ("sbvh_alpha", float("nan")), ("sbvh_budget", float("nan")),
+                       ("lds_treelet", -2), ("sbvh_c_trav", -1.0)):
         q = rtamd.upload_options(**{field: bad})
         rc = lib.rt_scene_upload_ex(hs.soa, hs.bvh, 0, C.byref(q), C.byref(C.c_void_p()))
         assert rc == abi.RT_ERR_INVALID, (field, rc)
@@ -110,3 +111,20 @@ def test_shard_rows_partition_the_image():
     for h, sh, n in [(1080, 16, 8), (1080, 16, 3), (17, 4, 2), (5, 16, 8)]:
         rows = sorted(sum((list(rtamd.shard_rows(h, sh, n, r)) for r in range(n)), []))
         assert rows == list(range(h))
+
+
+def test_zero_initialised_upload_options_are_valid():
+    # A C caller's zero-initialised rt_upload_options (`= {0}`, or a designated initialiser naming one
+    # field) must pass validation: zero sbvh_bins / sbvh_c_trav / collapse_c_tri / lds_treelet mean
+    # their defaults.  (No GPU here: the upload then fails at the HIP step, never as RT_ERR_INVALID.)
+    hs = rtamd.HostScene.generate("cornell")
+    hs.prepare()
+    lib = rtamd.hip_lib()
+    for tree in (abi.RT_TREE_SAH, abi.RT_TREE_SBVH, abi.RT_TREE_REFERENCE):
+        z = abi.UploadOptions()
+        z.device_tree = tree
+        h = C.c_void_p()
+        rc = lib.rt_scene_upload_ex(hs.soa, hs.bvh, 0, C.byref(z), C.byref(h))
+        assert rc != abi.RT_ERR_INVALID, lib.rt_last_error()
+        if rc == abi.RT_OK:
+            lib.rt_scene_free(h)

@@ -261,6 +261,9 @@ def test_tile_order_and_costs_change_no_pixel(nf):
     bad = order.copy()
     bad[0] = n_tiles
     assert lib.rt_debug_set_tile_order(dev._h, bad.ctypes.data_as(C.POINTER(C.c_uint)), n_tiles) != 0
+    dup = order.copy()
+    dup[0] = dup[1]   # in range, but a duplicate: not a permutation
+    assert lib.rt_debug_set_tile_order(dev._h, dup.ctypes.data_as(C.POINTER(C.c_uint)), n_tiles) != 0
     assert lib.rt_debug_set_tile_order(dev._h, None, 0) == 0
 
 
@@ -314,6 +317,34 @@ def test_concurrent_launches_on_streams_are_independent():
     torch.cuda.synchronize()
     for k in range(len(jobs)):
         assert np.array_equal(bufs[k].cpu().numpy().reshape(serial[k].shape), serial[k]), k
+
+
+def test_cost_order_maps_fenced_across_streams():
+    # The cost / order maps are shared by the scene's launches: launch q of a cost-ordered sequence
+    # builds the order of launch q + 1 in its drain.  Default (implicitly ordered) launches on stream
+    # A, then default launches on stream B (natural order: B is not the maps' stream), then explicit
+    # RT_FLAG_COST_ORDER launches on B (fenced on A's last map launch) and default launches on A again:
+    # every result equals the natural-order render bit for bit, with nothing synchronised in between.
+    import torch
+
+    hs, dev, _ = Case.get("office")
+    views = [_moved(hs.render_params(320, 180, 1), 0.03 * k) for k in range(4)]
+    for v in views:
+        v.out_format = rtamd.RT_OUT_RGB_F64
+    ref = [dev.render(_with_flags(v, rtamd.abi.RT_FLAG_NATURAL_ORDER))[0] for v in views]
+    A, B = torch.cuda.Stream(), torch.cuda.Stream()
+    plan = [(A, 0), (A, 0), (A, 0), (B, 0), (B, 0), (B, rtamd.abi.RT_FLAG_COST_ORDER),
+            (B, rtamd.abi.RT_FLAG_COST_ORDER), (A, 0), (A, 0), (B, 0), (A, 0), (A, 0)]
+    bufs = [torch.zeros(ref[0].size, dtype=torch.float64, device="cuda") for _ in plan]
+    want = [ref[k % len(views)] for k in range(len(plan))]
+    torch.cuda.synchronize()   # the buffers' fills are done before any launch
+    for k, (s, flags) in enumerate(plan):
+        with torch.cuda.stream(s):
+            dev.launch(_with_flags(views[k % len(views)], flags), bufs[k].data_ptr(), stats=False,
+                       stream=s.cuda_stream)
+    torch.cuda.synchronize()
+    for k, (b, r) in enumerate(zip(bufs, want)):
+        assert np.array_equal(b.cpu().numpy().reshape(r.shape), r), k
 
 
 def test_full_size_office_1080p_parity():

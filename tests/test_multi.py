@@ -123,6 +123,37 @@ def test_multi_driver_frames_equal_single_launches(gpu_available, office, nf, w,
 
 
 @pytest.mark.gpu
+def test_multi_driver_frames_async_three_batches(gpu_available, office):
+    # The timed path: stats=NULL (launches asynchronous, batch i + 1 renders while batch i is
+    # gathered and re-interleaved), more than two batches so every slot is reused after
+    # hipEventSynchronize(done) and its pinned output table is rewritten while later batches are in
+    # flight.  Batches hold at most RT_MAX_FRAMES (128) frames, so 2 x 128 + 5 frames give 3.
+    import torch
+    hs, _ = office
+    m = rtamd.MultiScene(hs, devices=(0,))
+    dev = rtamd.DeviceScene(hs, 0)
+    w, h, nf = 40, 24, 2 * rtamd.abi.RT_MAX_FRAMES + 5
+    base = hs.render_params(w, h, 1)
+    base.out_format = rtamd.RT_OUT_RGB_F64
+    cams = [rtamd.camera_orbit(base, 0.004 * f) for f in range(nf)]
+    outs = torch.full((nf, h, w, 3), float("nan"), dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    st, ms = m.render_frames(cams, [outs[f].data_ptr() for f in range(nf)], stripe_height=4, stats=False)
+    assert st is None and ms > 0
+    got = outs.cpu().numpy()
+    for f, cam in enumerate(cams):
+        ref, _ = dev.render(_natural(cam))
+        assert np.array_equal(got[f], ref), f
+    m.close()
+
+
+def _natural(p):
+    q = rtamd.abi.RenderParams.from_buffer_copy(p)
+    q.flags = rtamd.abi.RT_FLAG_NATURAL_ORDER
+    return q
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("nf", [1, 3])
 def test_multi_driver_two_gpus_equal_single_launch(gpu_available, office, nf):
     # The N > 1 path proper: grouped ncclGather of several GPUs' padded stripe buffers,
