@@ -24,13 +24,26 @@ def test_default_frames_per_launch():
 
 
 def test_valu_roof_from_committed_summary():
-    """The VALU-issue roof is read from the committed SQ counters of the workload: the office
-    summaries carry SQ_INSTS_VALU, and the fraction is instructions / kernel time / peak."""
+    """The VALU-issue roof is read from the committed SQ counters of the workload and priced per
+    class (MI355X_MICROARCH.md: 2 SIMD cycles per 32-bit wave64 instruction, 4 per fp64, 8 per fp64
+    transcendental) against 1024 SIMDs x 2.4 GHz x the kernel time per frame."""
     b = _bench()
     key = {"scene": "office", "tris": 0, "width": 1920, "height": 1080, "spp": 1, "tree": "sbvh",
            "sweep": 0.12, "adaptive": False, "analytic": False, "n_gpus": 1}
-    r = b.pmc_valu_roof(key, 128, 0.36e-3)
+    r = b.pmc_valu_roof(key, 20, 0.3408e-3)
     assert r is not None and r["source"].startswith("profiles/")
-    assert abs(r["frac"] - r["valu_insts_per_frame"] / 0.36e-3 / 1e9 / b.VALU_PEAK_GINSTS) < 1e-3
-    assert 0.0 < r["frac"] < 1.2 and (r["busy_frac"] is None or 0.0 < r["busy_frac"] < 1.1)
+    cycles = 2 * r["insts_b32"] + 4 * r["insts_f64"] + 8 * r["insts_trans_f64"]
+    assert abs(r["insts_b32"] + r["insts_f64"] + r["insts_trans_f64"] - r["valu_insts_per_frame"]) <= 3
+    assert abs(r["frac"] - cycles / (1024 * 2.4e9 * 0.3408e-3)) < 1e-3
+    assert 0.3 < r["frac"] < 0.7   # the office at the driver's shape: about half the issue capacity
     assert b.pmc_valu_roof(dict(key, scene="nonexistent"), 128, 0.36e-3) is None
+
+
+def test_metric_names_the_workload():
+    b = _bench()
+    a = types.SimpleNamespace(scene="office", width=1920, height=1080, spp=1, adaptive=False)
+    assert b.workload_label(a, 59670) == "Office 1920x1080 1spp"   # BASELINE.json's wording
+    a = types.SimpleNamespace(scene="random_tris", width=1920, height=1080, spp=1, adaptive=False)
+    assert b.workload_label(a, 10_000_000) == "random_tris 10M 1920x1080 1spp"
+    a = types.SimpleNamespace(scene="office", width=3840, height=2160, spp=4, adaptive=False)
+    assert b.workload_label(a, 59670) == "Office 3840x2160 16spp"
