@@ -115,6 +115,10 @@ def parse():
                          "reference median-split tree of BASELINE config 2, mybvh.cpp:375-539, and the SAH tree) "
                          "and report each with its upload / build seconds (tree_records); auto = on for one GPU, "
                          "scenes below 2^20 triangles, no --adaptive")
+    ap.add_argument("--reserve-cus", type=int, default=-2,
+                    help="rt_upload_options.reserve_cus: CUs each render launch leaves free (its grid on an internal "
+                         "CU-masked stream), so the RCCL gather of the previous launch runs beside it instead of "
+                         "after it (DESIGN.md §8); default 8 on N > 1, 0 on one GPU")
     ap.add_argument("--opt", action="append", default=[], metavar="FIELD=VALUE",
                     help="dev A/B: an rt_upload_options field (e.g. lds_treelet=9); pixels are identical")
     ap.add_argument("--analytic", action="store_true",
@@ -156,7 +160,7 @@ def main():
     gen = {"n_triangles": a.tris} if a.scene == "random_tris" and a.tris else {}
     host = rtamd.HostScene.generate(a.scene, **gen)
     build_s = host.prepare()
-    upload_opts = {k: (float(v) if "." in v else int(v)) for k, v in (o.split("=", 1) for o in a.opt)}
+    upload_opts = upload_options_for(a, n)
     t_up = time.perf_counter()
     gpu = rtamd.DeviceScene(host, device=dev, analytic=a.analytic or a.scene == "spheres",
                              tree=a.tree, **upload_opts)
@@ -465,6 +469,18 @@ def main():
     if n > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def upload_options_for(a, n):
+    """rt_upload_options fields of this run: --opt FIELD=VALUE (dev A/B), and reserve_cus -- by
+    default 8 CUs per GPU left free at N > 1 (one per XCD: room for RCCL's 256-VGPR gather waves
+    beside the persistent grid), none on one GPU."""
+    opts = {k: (float(v) if "." in v else int(v)) for k, v in (o.split("=", 1) for o in a.opt)}
+    if "reserve_cus" not in opts:
+        r = a.reserve_cus if a.reserve_cus >= -1 else (8 if n > 1 else 0)
+        if r:
+            opts["reserve_cus"] = r
+    return opts
 
 
 def tree_record(host, dev, a, upload_opts, tree, cams, F, fbuf, stream, rays_launch, timed_region):

@@ -215,7 +215,12 @@ typedef struct rt_upload_options {
   double sbvh_c_trav;    /* SBVH: node visit cost in triangle tests, for leaf termination (default 1.0;
                             0 = default) */
   double collapse_c_tri; /* RT_COLLAPSE_SAH: cost of a leaf slot per unit area (default 1.0; 0 = default) */
-  int reserved_[8];
+  int reserve_cus;       /* CUs each render launch leaves free for concurrent kernels (an RCCL gather of the
+                            previous launch: its 256-VGPR waves fit no single free block slot of the
+                            persistent grid): > 0 = the launches run on an internal stream
+                            whose CU mask excludes that many CUs (spread over the XCDs), the grid sized to
+                            the rest; 0 = none (default; rt_multi_create: 8 per GPU at N > 1); -1 = none */
+  int reserved_[7];
 } rt_upload_options;
 
 /* Fills *opt with the defaults listed above. */

@@ -156,6 +156,8 @@ void rt_multi_free(rt_multi* m) {
   delete m;
 }
 
+constexpr int kReserveCus = 8;   // one CU per XCD of an MI355X
+
 int rt_multi_create(const rt_scene_soa* soa, const rt_bvh_soa* bvh, const int* devices, int n_devices,
                     const rt_upload_options* opt, rt_multi** out) {
   if (!out || !devices || n_devices < 1) return fail(RT_ERR_INVALID, "rt_multi_create: bad argument");
@@ -167,7 +169,14 @@ int rt_multi_create(const rt_scene_soa* soa, const rt_bvh_soa* bvh, const int* d
   m->n = n_devices;
   m->devices.assign(devices, devices + n_devices);
   m->scenes.assign(n_devices, nullptr);
-  if (rt_scene_upload_multi(soa, bvh, devices, n_devices, opt, m->scenes.data()) != RT_OK) {
+  // N > 1: each GPU's render launches leave kReserveCus CUs free, so the RCCL gather of one batch
+  // runs beside the next batch's persistent kernel instead of waiting for its end;
+  // the caller's reserve_cus wins when set (-1: none)
+  rt_upload_options o;
+  if (opt) o = *opt;
+  else rt_upload_options_init(&o);
+  if (n_devices > 1 && o.reserve_cus == 0) o.reserve_cus = kReserveCus;
+  if (rt_scene_upload_multi(soa, bvh, devices, n_devices, &o, m->scenes.data()) != RT_OK) {
     const std::string e = rt_last_error();
     rt_multi_free(m);
     return fail(RT_ERR_HIP, "rt_multi_create: " + e);

@@ -1292,17 +1292,21 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
   }
           RT_CSWAP(0, 1) RT_CSWAP(2, 3) RT_CSWAP(0, 2) RT_CSWAP(1, 3) RT_CSWAP(1, 2)
 #undef RT_CSWAP
-          if (cnt == 0) {
-            cur = pop();
-          } else {
+          // next node: the nearest hit child; a first leaf is postponed and its next-nearest sibling
+          // taken directly (no push-then-pop through the ring); the rest is pushed far-first
+          const bool skip = (cnt > 0) && (v[0] & kLeaf) && pleaf == kDone;   // (children are never kDone)
+          if (skip) pleaf = v[0];
+          if (cnt > (skip ? 1 : 0)) {
             if (cnt > 3) push(v[3]);
             if (cnt > 2) push(v[2]);
-            if (cnt > 1) push(v[1]);
-            cur = v[0];
-          }
-          if ((cur & kLeaf) && cur != kDone && pleaf == kDone) {   // first leaf: postpone, keep going
-            pleaf = cur;
+            if (cnt > 1 && !skip) push(v[1]);
+            cur = skip ? v[1] : v[0];
+          } else {
             cur = pop();
+            if ((cur & kLeaf) && cur != kDone && pleaf == kDone) {   // first leaf: postpone, keep going
+              pleaf = cur;
+              cur = pop();
+            }
           }
           if ((wballot(pleaf == kDone) & wballot(cur != kDone)) == 0) break;   // every lane holds a leaf (one mask per compare)
         }
@@ -2073,6 +2077,7 @@ struct LaunchCtx {
   unsigned long long* d_wctr = nullptr;      // [nslots / 64][4] per-wave ray counts
   unsigned long long* d_tl = nullptr;        // [nslots / 64][kTlCap][kTlWords], allocated by the first TL launch
   hipEvent_t ev0 = nullptr, ev1 = nullptr;   // kernel start / end (timing, reuse fence)
+  hipEvent_t ev_in = nullptr;                // reserve_cus: the caller's stream joined to the launch stream
   long long waves = 0;                       // waves of the last launch (per-wave counter slots)
   int variant = -1;                          // kernel variant of the last launch (3: round timeline)
   bool used = false;
@@ -2138,6 +2143,13 @@ struct rt_scene {
   hipStream_t maps_stream = nullptr;
   hipEvent_t maps_ev = nullptr;
   double build_s = 0.0, copy_s = 0.0;   // rt_scene_upload_seconds
+  // rt_upload_options.reserve_cus: launches run on internal streams whose CU mask leaves that many
+  // CUs free, one per caller stream (at most kMaskedStreams, then shared round robin)
+  int reserve_cus = 0;
+  static constexpr int kMaskedStreams = 4;
+  hipStream_t masked[kMaskedStreams] = {};
+  hipStream_t masked_for[kMaskedStreams] = {};
+  int n_masked = 0;
 };
 
 namespace {
@@ -2225,6 +2237,7 @@ int upload_image(const SceneImage& I, const rt_upload_options& opt, int device, 
   }
   sc->bpc_cap = opt.blocks_per_cu;
   sc->grid_spare = opt.grid_spare;
+  sc->reserve_cus = opt.reserve_cus;   // bounded by the CU count below
   sc->delta = I.delta;
   for (int k = 0; k < 3; ++k) {
     sc->root_lo[k] = I.root_lo[k];
@@ -2234,6 +2247,7 @@ int upload_image(const SceneImage& I, const rt_upload_options& opt, int device, 
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) { rt_scene_free(sc); return fail(RT_ERR_HIP, "hipGetDeviceProperties failed"); }
   sc->n_cu = prop.multiProcessorCount;
+  sc->reserve_cus = std::max(0, std::min(sc->reserve_cus, sc->n_cu - 1));
   int max_blocks = 1;
   for (int v = 0; v < kNumVariants; ++v) {
     const int ring = variant_ring(v);
@@ -2294,6 +2308,7 @@ int resolve_options(const rt_upload_options* opt, rt_upload_options& o) {
   if (o.sbvh_c_trav == 0.0) o.sbvh_c_trav = d.sbvh_c_trav;
   if (o.collapse_c_tri == 0.0) o.collapse_c_tri = d.collapse_c_tri;
   if (o.lds_treelet < -1) return fail(RT_ERR_INVALID, "rt_scene_upload: lds_treelet must be >= -1");
+  if (o.reserve_cus < -1) return fail(RT_ERR_INVALID, "rt_scene_upload: reserve_cus must be >= -1");
   if (o.stack_ring != 0 && o.stack_ring != 8 && o.stack_ring != 16)
     return fail(RT_ERR_INVALID, "rt_scene_upload: stack_ring must be 0, 8 or 16");
   if (o.blocks_per_cu < 0 || o.grid_spare < 0 || o.build_threads < 0)
@@ -2415,6 +2430,33 @@ int read_counters(const LaunchCtx& C, unsigned long long* c) {
   return RT_OK;
 }
 
+// The CU-masked stream a launch from caller stream `caller` runs on (reserve_cus > 0): the mask
+// clears reserve_cus CUs spread evenly over the CU index range (one per XCD for 8 of 256), so a
+// concurrent kernel -- an RCCL gather whose waves need 256 VGPRs, more than any single free block
+// slot of the persistent grid offers -- finds whole CUs free.
+int masked_stream(rt_scene* sc, hipStream_t caller, hipStream_t* out) {
+  for (int i = 0; i < sc->n_masked && i < rt_scene::kMaskedStreams; ++i)
+    if (sc->masked_for[i] == caller) { *out = sc->masked[i]; return RT_OK; }
+  if (sc->n_masked >= rt_scene::kMaskedStreams) {   // more caller streams than masked ones: share
+    *out = sc->masked[(sc->n_masked++) % rt_scene::kMaskedStreams];
+    return RT_OK;
+  }
+  std::vector<uint32_t> mask((size_t)(sc->n_cu + 31) / 32, 0u);
+  for (int c = 0; c < sc->n_cu; ++c) mask[(size_t)c / 32] |= 1u << (c % 32);
+  const int stride = sc->n_cu / sc->reserve_cus;
+  for (int r = 0; r < sc->reserve_cus; ++r) {
+    const int c = r * stride + stride - 1;
+    mask[(size_t)c / 32] &= ~(1u << (c % 32));
+  }
+  hipStream_t s = nullptr;
+  HIP_TRY(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size() * 32u, mask.data()));
+  sc->masked[sc->n_masked] = s;
+  sc->masked_for[sc->n_masked] = caller;
+  sc->n_masked++;
+  *out = s;
+  return RT_OK;
+}
+
 // One render launch; list != nullptr: adaptive pass over the pixel ids list[0 .. *count)
 // (at most list_cap of them) of the full frame.
 // n_frames > 1 (rt_launch_frames): params p[0..n_frames) differ only in their camera vectors,
@@ -2457,6 +2499,18 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   P.prims = sc->d_prims; P.n_prims = sc->n_prims;
   LaunchCtx& C = sc->ctx[sc->next_ctx];
   const int ci = sc->next_ctx;
+  // reserve_cus: everything of this launch goes to the caller's CU-masked stream, joined to the
+  // caller's stream by events (in: after the caller's prior work; out: the caller waits for the end)
+  const hipStream_t caller = st;
+  if (sc->reserve_cus > 0) {
+    hipStream_t ks = nullptr;
+    const int mrc = masked_stream(sc, caller, &ks);
+    if (mrc != RT_OK) return mrc;
+    if (!C.ev_in) HIP_TRY(hipEventCreateWithFlags(&C.ev_in, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(C.ev_in, caller));
+    HIP_TRY(hipStreamWaitEvent(ks, C.ev_in, 0));
+    st = ks;
+  }
   P.ctr = C.d_ctr;
   P.heads = reinterpret_cast<unsigned long long*>(reinterpret_cast<unsigned char*>(C.d_ctr) + kHeadsOff);
   P.wctr = C.d_wctr;
@@ -2604,7 +2658,7 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   const long long waves_needed = (P.n_tiles * 64 + 63) / 64;
   int bpc = sc->blocks_per_cu[v];
   if (sc->bpc_cap > 0) bpc = std::min(bpc, sc->bpc_cap);   // a smaller persistent grid (upload option)
-  long long blocks = (long long)sc->n_cu * bpc;
+  long long blocks = (long long)(sc->n_cu - sc->reserve_cus) * bpc;
   blocks = std::max<long long>(1, std::min<long long>(blocks, (waves_needed + kBlock / 64 - 1) / (kBlock / 64)));
   blocks = std::min<long long>(blocks, (long long)(sc->nslots / kBlock));
   if (sc->grid_spare > 0)   // leave block slots to concurrent kernels (upload option)
@@ -2642,6 +2696,7 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
                             args, lds, st));
   }
   HIP_TRY(hipEventRecord(C.ev1, st));
+  if (st != caller) HIP_TRY(hipStreamWaitEvent(caller, C.ev1, 0));   // the caller's later work follows the launch
   if (cost_order || cost_debug) {   // this launch read / wrote the maps: the next map launch is fenced on it
     if (!sc->maps_ev) HIP_TRY(hipEventCreateWithFlags(&sc->maps_ev, hipEventDisableTiming));
     HIP_TRY(hipEventRecord(sc->maps_ev, st));
@@ -3067,6 +3122,10 @@ void rt_scene_free(rt_scene* sc) {
     if (c.ev1) (void)hipEventDestroy(c.ev1);
   }
   if (sc->maps_ev) (void)hipEventDestroy(sc->maps_ev);
+  for (LaunchCtx& c : sc->ctx)
+    if (c.ev_in) (void)hipEventDestroy(c.ev_in);
+  for (int i = 0; i < rt_scene::kMaskedStreams; ++i)
+    if (sc->masked[i]) (void)hipStreamDestroy(sc->masked[i]);
   delete sc;
 }
 

@@ -143,7 +143,8 @@ class UploadOptions(C.Structure):
                 ("lds_treelet", C.c_int), ("collapse", C.c_int), ("sbvh_leaf_max", C.c_int),
                 ("sbvh_bins", C.c_int), ("blocks_per_cu", C.c_int), ("grid_spare", C.c_int),
                 ("verbose", C.c_int), ("sbvh_alpha", C.c_double), ("sbvh_budget", C.c_double),
-                ("sbvh_c_trav", C.c_double), ("collapse_c_tri", C.c_double), ("reserved_", C.c_int * 8)]
+                ("sbvh_c_trav", C.c_double), ("collapse_c_tri", C.c_double), ("reserve_cus", C.c_int),
+                ("reserved_", C.c_int * 7)]
 
 
 RT_TREE_SAH, RT_TREE_REFERENCE, RT_TREE_SBVH = 0, 1, 2

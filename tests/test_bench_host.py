@@ -47,3 +47,14 @@ def test_metric_names_the_workload():
     assert b.workload_label(a, 10_000_000) == "random_tris 10M 1920x1080 1spp"
     a = types.SimpleNamespace(scene="office", width=3840, height=2160, spp=4, adaptive=False)
     assert b.workload_label(a, 59670) == "Office 3840x2160 16spp"
+
+
+def test_reserve_cus_at_n_above_one():
+    # N > 1: the render launches leave 8 CUs free for the RCCL gather; one GPU: none
+    b = _bench()
+    a = types.SimpleNamespace(opt=[], reserve_cus=-2)
+    assert b.upload_options_for(a, 1) == {}
+    assert b.upload_options_for(a, 8) == {"reserve_cus": 8}
+    assert b.upload_options_for(types.SimpleNamespace(opt=[], reserve_cus=0), 8) == {}
+    assert b.upload_options_for(types.SimpleNamespace(opt=["reserve_cus=4", "lds_treelet=9"], reserve_cus=-2), 8) == \
+        {"reserve_cus": 4, "lds_treelet": 9}

@@ -347,6 +347,39 @@ def test_cost_order_maps_fenced_across_streams():
         assert np.array_equal(b.cpu().numpy().reshape(r.shape), r), k
 
 
+def test_reserved_cus_change_no_pixel():
+    # rt_upload_options.reserve_cus: launches run on an internal CU-masked stream (whole CUs left
+    # free for a concurrent gather), joined to the caller's stream by events.  Pixels
+    # and ray counts are unchanged -- one frame, several frames, and launches on two caller streams
+    # in flight together -- and the caller's stream orders later work after the launch.
+    import torch
+
+    hs, dev, _ = Case.get("office")
+    res = rtamd.DeviceScene(hs, 0, reserve_cus=8)
+    p = hs.render_params(320, 180, 1)
+    p.out_format = rtamd.RT_OUT_RGB_F64
+    a, sa = dev.render(_with_flags(p, rtamd.abi.RT_FLAG_NATURAL_ORDER))
+    for _ in range(3):   # (ordered from the third launch on)
+        b, sb = res.render(p)
+        assert np.array_equal(a, b) and counts(sa) == counts(sb)
+    cams = [_moved(p, 0.03 * f) for f in range(5)]
+    refs = [dev.render(_with_flags(c, rtamd.abi.RT_FLAG_NATURAL_ORDER))[0] for c in cams]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = [[torch.zeros(a.size, dtype=torch.float64, device="cuda") for _ in cams] for _ in streams]
+    sums = [torch.zeros((), dtype=torch.float64, device="cuda") for _ in streams]
+    torch.cuda.synchronize()
+    for k, s in enumerate(streams):
+        with torch.cuda.stream(s):
+            res.launch_frames(cams, [o.data_ptr() for o in outs[k]], stream=s.cuda_stream)
+            sums[k] += outs[k][-1].sum()   # caller-stream work after the launch sees its output
+    torch.cuda.synchronize()
+    for k in range(len(streams)):
+        for f, r in enumerate(refs):
+            assert np.array_equal(outs[k][f].cpu().numpy().reshape(r.shape), r), (k, f)
+        assert float(sums[k]) == float(r.sum())
+    res.close()
+
+
 def test_full_size_office_1080p_parity():
     # BASELINE config 2 at full size: whole-frame fp64 parity and exact ray counts.
     hs, dev, orc = Case.get("office")
