@@ -376,7 +376,7 @@ def test_reserved_cus_change_no_pixel():
     for k in range(len(streams)):
         for f, r in enumerate(refs):
             assert np.array_equal(outs[k][f].cpu().numpy().reshape(r.shape), r), (k, f)
-        assert float(sums[k]) == float(r.sum())
+        assert abs(float(sums[k]) - float(r.sum())) < 1e-6 * r.size   # (different summation order)
     res.close()
 
 
