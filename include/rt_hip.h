@@ -344,8 +344,7 @@ int rt_last_kernel_ms(rt_scene* scene, float* ms);
  * wave-level node / leaf iteration (summed), triangle tests in leaves of > 4,
  * node iterations served from the LDS treelet; word 31 = watchdog flag; words
  * [32,35) = global-node iterations with one node for the whole wave, distinct
- * nodes of global-node iterations (summed), leaf iterations with one record; words 35, 36 =
- * occluder-cache tests (wave-level) and the shadow rays the cache occluded.
+ * nodes of global-node iterations (summed), leaf iterations with one record.
  * Returns the number of words copied (at most 40). */
 int rt_debug_counters(rt_scene* scene, unsigned long long* out, int n);
 

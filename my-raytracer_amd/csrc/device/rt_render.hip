@@ -73,13 +73,8 @@ constexpr int kShortStack = 8;
 // LDS instead of the vector-L1 path.  0 disables.
 // LDS per thread: kSlotDoubles fp64 slot words, task + visibility words, the stack ring
 constexpr int kSlotDoubles = 10;
-// occluder cache: per wave and light (the first kOccLights lights), the record that last occluded a
-// shadow ray
-constexpr int kOccLights = RT_MAX_LIGHTS;
-constexpr int kOccBytes = (kBlock / 64) * kOccLights * 4;
-// fills the CU's 160 KB at 4 blocks with the slots, ring, lights, pool, occluder cache (71 nodes)
-constexpr int kTopNodes =
-    (40960 - kBlock * (kSlotDoubles * 8 + (2 + kShortStack) * 4) - RT_MAX_LIGHTS * 48 - 64 - kOccBytes) / 128;
+// fills the CU's 160 KB at 4 blocks with the slots, ring, lights, pool (73 nodes)
+constexpr int kTopNodes = (40960 - kBlock * (kSlotDoubles * 8 + (2 + kShortStack) * 4) - RT_MAX_LIGHTS * 48 - 64) / 128;
 constexpr int kStackMask = kShortStack - 1;
 // Tail compaction: once the work queue is empty, a wave with at most kDonateMax
 // pixels in flight hands them to the other waves of its block and exits, so the last pixels
@@ -167,7 +162,6 @@ enum : int {
   CD_FETCH_CYCLES, CD_OUTER_ITERS, CD_TRAV_ROUNDS, CD_TRAV_ROUND_LANES, CD_SPILLS, CD_NODE_LINES,
   CD_LEAF_LINES, CD_BIG_LEAF_TESTS, CD_NODE_LDS_ITERS, CD_GUARD = 31,   // CD_GUARD: a wave hit the iteration guard
   CD_GNODE_UNIFORM = 32, CD_GNODE_DISTINCT, CD_LEAF_UNIFORM,
-  CD_OCC_TESTS = 35, CD_OCC_HITS,   // occluder cache: wave-level tests, rays it occluded
   CT_ORDER_JOBS = 39   // cost-ordered launches: order / zeroing jobs claimed by blocks that finished
 };
 // Watchdogs (never reached by a correct kernel): the persistent loop, and the wave-level
@@ -626,9 +620,6 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
   unsigned long long* pool_mask = reinterpret_cast<unsigned long long*>(lds_raw + P.pool_off + 8);
   // heads this block found exhausted (skipped without an atomic)
   uint32_t* pool_exh = reinterpret_cast<uint32_t*>(lds_raw + P.pool_off + 8 + 8 * (kBlock / 64));
-  // this wave's occluder-cache entries (kDone = none)
-  uint32_t* occ = reinterpret_cast<uint32_t*>(lds_raw + P.pool_off + kPoolBytes) + (threadIdx.x >> 6) * kOccLights;
-  if ((threadIdx.x & 63) < kOccLights) occ[threadIdx.x & 63] = kDone;
   if (threadIdx.x == 0) {
     *pool_live = kBlock / 64;
     for (int w = 0; w < kBlock / 64; ++w) pool_mask[w] = 0ull;
@@ -709,7 +700,6 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
   unsigned long long d_node_it = 0, d_node_ln = 0, d_leaf_it = 0, d_leaf_ln = 0;
   unsigned long long d_trav = 0, d_shade = 0, d_fetch = 0, d_outer = 0, d_round_it = 0, d_round_ln = 0;
   unsigned long long d_spills = 0, d_node_lines = 0, d_leaf_lines = 0, d_big_leaf = 0, d_node_lds = 0, d_dummy = 0, d_gn_uni = 0, d_gn_dist = 0, d_leaf_uni = 0;
-  unsigned long long d_occ_tests = 0, c_occ_hits = 0;
   unsigned long long w_start = STATS ? __builtin_amdgcn_s_memrealtime() : 0ull, w_refill = 0, w_pixels = 0;
   unsigned long long t_stamp = 0;
   // TL (round timeline, diagnostics): rounds recorded by this wave, the round's start stamp and
@@ -919,13 +909,11 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
       D3 ro = d3(lds_d[0 * kBlock + src], lds_d[1 * kBlock + src], lds_d[2 * kBlock + src]);
       D3 rd = d3(lds_d[3 * kBlock + src], lds_d[4 * kBlock + src], lds_d[5 * kBlock + src]);
       double tlim = lds_d[6 * kBlock + src];
-      int sj = kOccLights;   // shadow rays: the light (its occluder-cache entry when < kOccLights)
       if (anyhit) {
         // a shadow ray (mytracer.cpp:589-600) for light j of the owner's bounce, derived from the
         // closest-hit ray and hit distance kept in the owner's slot: the same operations, in the
         // same order, as the emission of an explicit ray (emit_ray normalises the direction again)
         const int j = (state == ST_SHADOW) ? light : (int)((htask >> 11) & 0xFFFFFu);
-        sj = j;
         const D3 hp = add(ro, scl(tlim, rd));
         const D3 to_l = sub(light_of(j).pos, hp);
         double nl;   // |to_l|: the light distance, the same sqrt as the normalisation's
@@ -962,66 +950,6 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
           tlim = t;
           best = kPrimHit | k;
           best_slot = -1;
-        }
-      }
-      const D3 c3 = d3(-rd.x, -rd.y, -rd.z);
-      // Mesh::intersect_triangle (mymesh.cpp:190-215) on record T: the same fp64 S, Da, Db, Dt as the
-      // CPU (bit-identical operands and operation order).  Division-free early rejections first: they
-      // fire only where the CPU's rounded quotients certainly fail the same test (margins in
-      // DESIGN.md §4), so accept decisions are unchanged.  True when the ray hits T inside the
-      // window (t > 1e-5; t < tlim for any-hit rays, t <= tlim for closest-hit ones), with t and the
-      // barycentrics alpha, beta.
-      auto tri_hit = [&](const TriOps& T, double& t, double& alpha, double& beta) -> bool {
-        const D3 c4 = sub(ro, T.p2);
-        const double S = det3(T.e1, T.e2, c3);
-        if (!(fabs(S) >= 1e-10)) return false;
-        const double Da = det3(c4, T.e2, c3);
-        const double Db = det3(T.e1, c4, c3);
-        const double sS = S > 0.0 ? 1.0 : -1.0;
-        const double aS = fabs(S);
-        const double ua = Da * sS, ub = Db * sS;                       // sign-normalised numerators
-        const double tiny = aS * 0x1p-1000, big = aS * (1.0 + 0x1p-48);
-        const bool out = (ua < 0.0 && -ua >= tiny) || (ub < 0.0 && -ub >= tiny) || ua > big || ub > big ||
-                         (Da + Db - S) * sS > 0x1p-40 * (fabs(Da) + fabs(Db) + aS);
-        if (out) return false;
-        const double Dt = det3(T.e1, T.e2, c4);
-        // (t's division shared with alpha / beta's reciprocal: -0.9 %, more live registers)
-        t = Dt / S;
-        const bool cand = anyhit ? (t < tlim) : (t <= tlim);
-        if (!(t > 1e-5 && cand)) return false;
-        // alpha, beta: one reciprocal of S for the two quotients where that is bit-identical:
-        // |S| >= 1e-10 here and |Da|, |Db| <= |S|(1 + 2^-48) (the early rejections), so with
-        // |Da|, |Db| >= |S| 2^-900 and |S| < 2^1000 no operand or quotient is denormal, zero or
-        // near an exponent limit
-        const double lim = aS * 0x1p-900;
-        const bool fab = !STATS && !TL && fabs(Da) >= lim && fabs(Db) >= lim && aS < 0x1p1000;
-        if (fab) {
-          const double r = rcp_refined(S);
-          alpha = div_by(Da, S, r);
-          beta = div_by(Db, S, r);
-        } else {
-          alpha = Da / S;
-          beta = Db / S;
-        }
-        const double gamma = (1.0 - alpha - beta);
-        return (0.0 <= alpha && alpha <= 1.0) && (0.0 <= beta && beta <= 1.0) && (0.0 <= gamma && gamma <= 1.0);
-      };
-      // Occluder cache (4-wide variants): a shadow ray first tests the triangle that last occluded a
-      // shadow ray to the same light in this wave (neighbouring pixels of a tile are often shadowed by
-      // the same triangle).  If it occludes, the ray is occluded and skips the BVH: the any-hit result
-      // is "some triangle in (1e-5, light distance) passes the exact test", whichever one is found,
-      // so pixels and ray counts are unchanged.
-      if constexpr (WIDTH == 4) {
-        if (anyhit && busy && !shadow_hit && !resumed && sj < kOccLights) {
-          const uint32_t oc = occ[sj];
-          if (oc != kDone) {
-            double t_, a_, b_;
-            if (STATS) wave_tick(d_occ_tests, d_dummy, lane);
-            if (tri_hit(load_tri(P.tris, oc), t_, a_, b_)) {
-              shadow_hit = true;
-              if (STATS) c_occ_hits++;
-            }
-          }
         }
       }
       if (busy && P.n_gnodes > 0 && !shadow_hit) {   // conservative fp32 box ray (oracle/rt_oracle.c gray_setup)
@@ -1131,6 +1059,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
         sqlim = sq + kRingB;
         return spill[(size_t)(sq / kSW) * P.nslots];
       };
+      const D3 c3 = d3(-rd.x, -rd.y, -rd.z);
 
       // Watchdog of the traversal loops that could cycle on a corrupt hierarchy (the round loop
       // and the node loops): each counts its own wave-level iterations in a counter that lives
@@ -1165,23 +1094,63 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
             }
             const TriOps T = load_tri(P.tris, rec);
             const int slot = (int)(T.meta & kSlotMask);
-            double t, alpha, beta;
-            if (tri_hit(T, t, alpha, beta)) {
-              if (anyhit) {
-                shadow_hit = true;
-                occluded = true;
-                if (WIDTH == 4 && sj < kOccLights) occ[sj] = rec;   // the wave's occluder for this light
-                break;
-              }
-              if (t < tlim || slot < best_slot) {   // ties: smallest slot (mybvh.cpp:169 visit order)
-                tlim = t;
-                best = (int)rec;
-                best_slot = slot;
-                hi_c = round_up_f(tlim - t_off);
-                // hit attributes for shading (slot aux words: free while a closest-hit ray is in flight)
-                *R.a[0] = alpha;
-                *R.a[1] = beta;
-                *R.a[2] = __longlong_as_double((long long)T.mesh);
+            // Mesh::intersect_triangle (mymesh.cpp:190-215): the same fp64 S, Da, Db, Dt as
+            // the CPU (bit-identical operands and operation order).  Division-free early
+            // rejections first: they fire only where the CPU's rounded quotients certainly
+            // fail the same test (margins in DESIGN.md §4), so accept decisions are unchanged.
+            const D3 c4 = sub(ro, T.p2);
+            const double S = det3(T.e1, T.e2, c3);
+            if (fabs(S) >= 1e-10) {
+              const double Da = det3(c4, T.e2, c3);
+              const double Db = det3(T.e1, c4, c3);
+              const double sS = S > 0.0 ? 1.0 : -1.0;
+              const double aS = fabs(S);
+              const double ua = Da * sS, ub = Db * sS;                       // sign-normalised numerators
+              const double tiny = aS * 0x1p-1000, big = aS * (1.0 + 0x1p-48);
+              const bool out = (ua < 0.0 && -ua >= tiny) || (ub < 0.0 && -ub >= tiny) || ua > big || ub > big ||
+                               (Da + Db - S) * sS > 0x1p-40 * (fabs(Da) + fabs(Db) + aS);
+              if (!out) {
+                const double Dt = det3(T.e1, T.e2, c4);
+                // (t's division shared with alpha / beta's reciprocal: -0.9 %, more live registers)
+                const double t = Dt / S;
+                const bool cand = anyhit ? (t < tlim) : (t <= tlim);
+                if (t > 1e-5 && cand) {
+                  double alpha, beta;
+                  // alpha, beta: one reciprocal of S for the two quotients where that is bit-identical:
+                  // |S| >= 1e-10 here and |Da|, |Db| <= |S|(1 + 2^-48) (the early rejections), so with
+                  // |Da|, |Db| >= |S| 2^-900 and |S| < 2^1000 no operand or quotient is denormal, zero or
+                  // near an exponent limit
+                  const double lim = aS * 0x1p-900;
+                  const bool fab = !STATS && !TL && fabs(Da) >= lim && fabs(Db) >= lim && aS < 0x1p1000;
+                  if (fab) {
+                    const double r = rcp_refined(S);
+                    alpha = div_by(Da, S, r);
+                    beta = div_by(Db, S, r);
+                  } else {
+                    alpha = Da / S;
+                    beta = Db / S;
+                  }
+                  const double gamma = (1.0 - alpha - beta);
+                  const bool inside = (0.0 <= alpha && alpha <= 1.0) && (0.0 <= beta && beta <= 1.0) &&
+                                      (0.0 <= gamma && gamma <= 1.0);
+                  if (inside) {
+                    if (anyhit) {
+                      shadow_hit = true;
+                      occluded = true;
+                      break;
+                    }
+                    if (t < tlim || slot < best_slot) {   // ties: smallest slot (mybvh.cpp:169 visit order)
+                      tlim = t;
+                      best = (int)rec;
+                      best_slot = slot;
+                      hi_c = round_up_f(tlim - t_off);
+                      // hit attributes for shading (slot aux words: free while a closest-hit ray is in flight)
+                      *R.a[0] = alpha;
+                      *R.a[1] = beta;
+                      *R.a[2] = __longlong_as_double((long long)T.mesh);
+                    }
+                  }
+                }
               }
             }
             if (T.meta & (WIDTH == 2 ? kLastRef : kLastDev)) break;
@@ -1323,21 +1292,17 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
   }
           RT_CSWAP(0, 1) RT_CSWAP(2, 3) RT_CSWAP(0, 2) RT_CSWAP(1, 3) RT_CSWAP(1, 2)
 #undef RT_CSWAP
-          // next node: the nearest hit child; a first leaf is postponed and its next-nearest sibling
-          // taken directly (no push-then-pop through the ring); the rest is pushed far-first
-          const bool skip = (cnt > 0) && (v[0] & kLeaf) && pleaf == kDone;   // (children are never kDone)
-          if (skip) pleaf = v[0];
-          if (cnt > (skip ? 1 : 0)) {
+          if (cnt == 0) {
+            cur = pop();
+          } else {
             if (cnt > 3) push(v[3]);
             if (cnt > 2) push(v[2]);
-            if (cnt > 1 && !skip) push(v[1]);
-            cur = skip ? v[1] : v[0];
-          } else {
+            if (cnt > 1) push(v[1]);
+            cur = v[0];
+          }
+          if ((cur & kLeaf) && cur != kDone && pleaf == kDone) {   // first leaf: postpone, keep going
+            pleaf = cur;
             cur = pop();
-            if ((cur & kLeaf) && cur != kDone && pleaf == kDone) {   // first leaf: postpone, keep going
-              pleaf = cur;
-              cur = pop();
-            }
           }
           if ((wballot(pleaf == kDone) & wballot(cur != kDone)) == 0) break;   // every lane holds a leaf (one mask per compare)
         }
@@ -1847,10 +1812,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
     const unsigned long long g = wave_sum(d_spills), h = wave_sum(d_node_lines), q = wave_sum(d_leaf_lines);
     const unsigned long long r = wave_sum(d_big_leaf), t = wave_sum(d_node_lds);
     const unsigned long long gu = wave_sum(d_gn_uni), gd = wave_sum(d_gn_dist), lu = wave_sum(d_leaf_uni);
-    const unsigned long long ot = wave_sum(d_occ_tests), oh = wave_sum(c_occ_hits);
     if (lane == 0) {
-      atomicAdd(&P.ctr[CD_OCC_TESTS], ot);
-      atomicAdd(&P.ctr[CD_OCC_HITS], oh);
       atomicAdd(&P.ctr[CD_NODE_LDS_ITERS], t);
       atomicAdd(&P.ctr[CD_GNODE_UNIFORM], gu);
       atomicAdd(&P.ctr[CD_GNODE_DISTINCT], gd);
@@ -2085,8 +2047,7 @@ size_t lds_bytes(int /*stack_words*/, int ring = kShortStack) {
 }
 // ... plus the top treelet (n_top 128-B nodes) after it
 size_t lds_bytes_total(int stack_words, int n_top, int ring = kShortStack) {
-  return lds_bytes(stack_words, ring) + (size_t)n_top * sizeof(GNode4) + RT_MAX_LIGHTS * 6 * sizeof(double) + kPoolBytes +
-         kOccBytes;
+  return lds_bytes(stack_words, ring) + (size_t)n_top * sizeof(GNode4) + RT_MAX_LIGHTS * 6 * sizeof(double) + kPoolBytes;
 }
 // treelet nodes that fit next to a ring of the given size in a block's 40 KB (kTopNodes beside the
 // 8-entry ring)
@@ -2466,9 +2427,9 @@ int read_counters(const LaunchCtx& C, unsigned long long* c) {
 }
 
 // The CU-masked stream a launch from caller stream `caller` runs on (reserve_cus > 0): the mask
-// clears reserve_cus CUs spread evenly over the CU index range (one per XCD for 8 of 256), so a
-// concurrent kernel -- an RCCL gather whose waves need 256 VGPRs, more than any single free block
-// slot of the persistent grid offers -- finds whole CUs free.
+// clears reserve_cus CUs spread evenly over the CU index range, so a concurrent kernel -- an RCCL
+// gather whose waves need 256 VGPRs, more than any single free block slot of the persistent grid
+// offers -- finds whole CUs free.
 int masked_stream(rt_scene* sc, hipStream_t caller, hipStream_t* out) {
   for (int i = 0; i < sc->n_masked && i < rt_scene::kMaskedStreams; ++i)
     if (sc->masked_for[i] == caller) { *out = sc->masked[i]; return RT_OK; }

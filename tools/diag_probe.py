@@ -27,8 +27,6 @@ for flags, name in [(rtamd.RT_FLAG_WIDE_STATS, "4-wide"), (rtamd.RT_FLAG_TRAVERS
     print(f"  trav rounds: {d['trav_rounds']}, lanes active {d['trav_round_lanes']/(64*max(1,d['trav_rounds'])):.3f}; outer iters {d['outer_iters']}")
     print(f"  cycles: trav {d['trav_cycles']/tot:.3f} shade {d['shade_cycles']/tot:.3f} fetch {d['fetch_cycles']/tot:.3f} (total wave-cycles {tot:.3e})")
     print(f"  stack spills {d['stack_spills']} ({d['stack_spills']/rays:.3f} per ray)")
-    print(f"  occluder cache: {d['occ_tests']} wave-level tests, {d['occ_hits']} shadow rays occluded by it "
-          f"({d['occ_hits']/max(1, st.shadow_rays):.3f} of {st.shadow_rays} shadow rays)")
     print(f"  per ray: node wave-iters {d['node_iters']*64/rays:.1f}  leaf wave-iters {d['leaf_iters']*64/rays:.1f}")
     it = d['node_iters'] + d['leaf_iters']
     print(f"  trav cycles per wave-iteration {d['trav_cycles']/max(1,it):.0f}; trav rounds {d['trav_rounds']}, "

@@ -8,7 +8,7 @@ set -e -o pipefail
 TAG=${1:?tag}; shift
 O=gpurun_out
 export TMPDIR=/tmp
-B="python bench.py --no-cpu-baseline $*"
+B="python bench.py --no-cpu-baseline --tree-record off $*"
 timeout -k 10 300 $B > $O/bench_$TAG.json 2> $O/bench_$TAG.err
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$TAG -o run -- $B > $O/prof_$TAG.log 2>&1
 # the traced run prints its own bench line: compare per-shape kernel durations with its HIP events
