@@ -118,7 +118,7 @@ def parse():
     ap.add_argument("--reserve-cus", type=int, default=-2,
                     help="rt_upload_options.reserve_cus: CUs each render launch leaves free (its grid on an internal "
                          "CU-masked stream), so the RCCL gather of the previous launch runs beside it instead of "
-                         "after it (DESIGN.md §8); default 8 on N > 1, 0 on one GPU")
+                         "after it (DESIGN.md §8); default 32 (one XCD's worth) on N > 1, 0 on one GPU")
     ap.add_argument("--opt", action="append", default=[], metavar="FIELD=VALUE",
                     help="dev A/B: an rt_upload_options field (e.g. lds_treelet=9); pixels are identical")
     ap.add_argument("--analytic", action="store_true",
@@ -473,11 +473,11 @@ def main():
 
 def upload_options_for(a, n):
     """rt_upload_options fields of this run: --opt FIELD=VALUE (dev A/B), and reserve_cus -- by
-    default 8 CUs per GPU left free at N > 1 (one per XCD: room for RCCL's 256-VGPR gather waves
-    beside the persistent grid), none on one GPU."""
+    default 32 CUs per GPU left free at N > 1 (one XCD's worth: the smallest reservation beside
+    which a kernel of RCCL's gather shape ran), none on one GPU."""
     opts = {k: (float(v) if "." in v else int(v)) for k, v in (o.split("=", 1) for o in a.opt)}
     if "reserve_cus" not in opts:
-        r = a.reserve_cus if a.reserve_cus >= -1 else (8 if n > 1 else 0)
+        r = a.reserve_cus if a.reserve_cus >= -1 else (32 if n > 1 else 0)
         if r:
             opts["reserve_cus"] = r
     return opts

@@ -218,8 +218,10 @@ typedef struct rt_upload_options {
   int reserve_cus;       /* CUs each render launch leaves free for concurrent kernels (an RCCL gather of the
                             previous launch: its 256-VGPR waves fit no single free block slot of the
                             persistent grid): > 0 = the launches run on an internal stream
-                            whose CU mask excludes that many CUs (spread over the XCDs), the grid sized to
-                            the rest; 0 = none (default; rt_multi_create: 8 per GPU at N > 1); -1 = none */
+                            whose CU mask clears the first reserve_cus CUs, the grid sized to the rest
+                            (32 = one XCD's worth: the smallest reservation a 256-VGPR kernel was
+                            measured to run beside); 0 = none (default; rt_multi_create: 32 per GPU at
+                            N > 1); -1 = none */
   int reserved_[7];
 } rt_upload_options;
 

@@ -156,7 +156,7 @@ void rt_multi_free(rt_multi* m) {
   delete m;
 }
 
-constexpr int kReserveCus = 8;   // one CU per XCD of an MI355X
+constexpr int kReserveCus = 32;   // one XCD's worth of an MI355X
 
 int rt_multi_create(const rt_scene_soa* soa, const rt_bvh_soa* bvh, const int* devices, int n_devices,
                     const rt_upload_options* opt, rt_multi** out) {
@@ -170,7 +170,8 @@ int rt_multi_create(const rt_scene_soa* soa, const rt_bvh_soa* bvh, const int* d
   m->devices.assign(devices, devices + n_devices);
   m->scenes.assign(n_devices, nullptr);
   // N > 1: each GPU's render launches leave kReserveCus CUs free, so the RCCL gather of one batch
-  // runs beside the next batch's persistent kernel instead of waiting for its end;
+  // runs beside the next batch's persistent kernel instead of waiting for its end (a 256-VGPR kernel
+  // fits beside the grid only with a whole XCD's worth free: DESIGN.md §8);
   // the caller's reserve_cus wins when set (-1: none)
   rt_upload_options o;
   if (opt) o = *opt;

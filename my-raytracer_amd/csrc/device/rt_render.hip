@@ -2427,9 +2427,12 @@ int read_counters(const LaunchCtx& C, unsigned long long* c) {
 }
 
 // The CU-masked stream a launch from caller stream `caller` runs on (reserve_cus > 0): the mask
-// clears reserve_cus CUs spread evenly over the CU index range, so a concurrent kernel -- an RCCL
-// gather whose waves need 256 VGPRs, more than any single free block slot of the persistent grid
-// offers -- finds whole CUs free.
+// clears the first reserve_cus CU bits, so a concurrent kernel -- an RCCL gather whose waves need
+// 256 VGPRs, more than any single free block slot of the persistent grid offers -- finds whole CUs
+// free.  Measured with a kernel of RCCL's resource shape (tools/cumask_probe.py,
+// profiles/r04/r04e_cumask.txt): it runs beside the grid only when the first 32 bits are clear
+// (one XCD's worth); 8 or 16 CUs, or 32 spread over the mask, leave it waiting for the grid's end
+// (DESIGN.md §8).
 int masked_stream(rt_scene* sc, hipStream_t caller, hipStream_t* out) {
   for (int i = 0; i < sc->n_masked && i < rt_scene::kMaskedStreams; ++i)
     if (sc->masked_for[i] == caller) { *out = sc->masked[i]; return RT_OK; }
@@ -2438,12 +2441,7 @@ int masked_stream(rt_scene* sc, hipStream_t caller, hipStream_t* out) {
     return RT_OK;
   }
   std::vector<uint32_t> mask((size_t)(sc->n_cu + 31) / 32, 0u);
-  for (int c = 0; c < sc->n_cu; ++c) mask[(size_t)c / 32] |= 1u << (c % 32);
-  const int stride = sc->n_cu / sc->reserve_cus;
-  for (int r = 0; r < sc->reserve_cus; ++r) {
-    const int c = r * stride + stride - 1;
-    mask[(size_t)c / 32] &= ~(1u << (c % 32));
-  }
+  for (int c = sc->reserve_cus; c < sc->n_cu; ++c) mask[(size_t)c / 32] |= 1u << (c % 32);
   hipStream_t s = nullptr;
   HIP_TRY(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size() * 32u, mask.data()));
   sc->masked[sc->n_masked] = s;

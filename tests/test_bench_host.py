@@ -50,11 +50,11 @@ def test_metric_names_the_workload():
 
 
 def test_reserve_cus_at_n_above_one():
-    # N > 1: the render launches leave 8 CUs free for the RCCL gather; one GPU: none
+    # N > 1: the render launches leave 32 CUs free for the RCCL gather; one GPU: none
     b = _bench()
     a = types.SimpleNamespace(opt=[], reserve_cus=-2)
     assert b.upload_options_for(a, 1) == {}
-    assert b.upload_options_for(a, 8) == {"reserve_cus": 8}
+    assert b.upload_options_for(a, 8) == {"reserve_cus": 32}
     assert b.upload_options_for(types.SimpleNamespace(opt=[], reserve_cus=0), 8) == {}
     assert b.upload_options_for(types.SimpleNamespace(opt=["reserve_cus=4", "lds_treelet=9"], reserve_cus=-2), 8) == \
         {"reserve_cus": 4, "lds_treelet": 9}

@@ -355,7 +355,7 @@ def test_reserved_cus_change_no_pixel():
     import torch
 
     hs, dev, _ = Case.get("office")
-    res = rtamd.DeviceScene(hs, 0, reserve_cus=8)
+    res = rtamd.DeviceScene(hs, 0, reserve_cus=32)
     p = hs.render_params(320, 180, 1)
     p.out_format = rtamd.RT_OUT_RGB_F64
     a, sa = dev.render(_with_flags(p, rtamd.abi.RT_FLAG_NATURAL_ORDER))

@@ -29,10 +29,10 @@ x = torch.ones(24 * 1024 * 1024, device="cuda")
 y = torch.empty_like(x)
 sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
 res = {}
-configs = [("base", {}), ("grid_spare=64", {"grid_spare": 64}), ("reserve_cus=8", {"reserve_cus": 8}),
-           ("reserve_cus=16", {"reserve_cus": 16})]
+configs = [("base", {}), ("grid_spare=64", {"grid_spare": 64})] + \
+    [(f"reserve_cus={r}", {"reserve_cus": r}) for r in (int(x) for x in (sys.argv[1:] or ["8", "16"]))]
 scenes = {name: rtamd.DeviceScene(host, 0, **kw) for name, kw in configs}
-for rep in range(5):
+for rep in range(3):
     for name, _ in configs:
         gpu = scenes[name]
         torch.cuda.synchronize()
