@@ -72,9 +72,20 @@ constexpr int kShortStack = 8;
 // into each block's LDS; a node iteration whose active lanes all sit in the treelet reads
 // LDS instead of the vector-L1 path.  0 disables.
 // LDS per thread: kSlotDoubles fp64 slot words, task + visibility words, the stack ring
+// LDS pool: live-wave count, one 64-bit lane mask per wave of the block, exhausted heads; then per
+// wave its work reservation {next, end, head position last seen} (3 u64)
+constexpr int kResOff = 48;
+constexpr int kPoolBytes = kResOff + 24 * (kBlock / 64);
+static_assert(8 + 8 * (kBlock / 64) + 4 <= kResOff, "compaction pool does not fit");
+// Work reservations: a refilling wave claims kChunk work items from its head with one device atomic
+// while the head's range has more than kChunkGuard items left, keeps the surplus in its LDS words
+// and serves later refills from them (no atomic); near a range's end it claims exactly what it needs
+// (the surplus of 512 waves per head would otherwise leave some waves a tile or two behind at the end)
+constexpr long long kChunk = 128;
+constexpr long long kChunkGuard = 2 * 512 * kChunk;
 constexpr int kSlotDoubles = 10;
-// fills the CU's 160 KB at 4 blocks with the slots, ring, lights, pool (73 nodes)
-constexpr int kTopNodes = (40960 - kBlock * (kSlotDoubles * 8 + (2 + kShortStack) * 4) - RT_MAX_LIGHTS * 48 - 64) / 128;
+// fills the CU's 160 KB at 4 blocks with the slots, ring, lights, pool (72 nodes)
+constexpr int kTopNodes = (40960 - kBlock * (kSlotDoubles * 8 + (2 + kShortStack) * 4) - RT_MAX_LIGHTS * 48 - kPoolBytes) / 128;
 constexpr int kStackMask = kShortStack - 1;
 // Tail compaction: once the work queue is empty, a wave with at most kDonateMax
 // pixels in flight hands them to the other waves of its block and exits, so the last pixels
@@ -84,8 +95,6 @@ constexpr int kStackMask = kShortStack - 1;
 constexpr int kDonateMax = 24;   // (0 = tail compaction off: -2.8 % batched, -1.4 % one frame)
 constexpr int kMigWords = 8;
 static_assert(kMigWords <= kShortStack, "migration words travel in the stack ring entries");
-constexpr int kPoolBytes = 64;   // LDS: live-wave count, one 64-bit lane mask per wave of the block, exhausted heads
-static_assert(8 + 8 * (kBlock / 64) + 4 <= kPoolBytes, "compaction pool does not fit");
 static_assert((kShortStack & kStackMask) == 0, "the stack ring must be a power of two");
 
 // Lane states.  Owners carry a pixel (CLOSEST: closest-hit ray in flight; SHADOW: a
@@ -620,6 +629,10 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
   unsigned long long* pool_mask = reinterpret_cast<unsigned long long*>(lds_raw + P.pool_off + 8);
   // heads this block found exhausted (skipped without an atomic)
   uint32_t* pool_exh = reinterpret_cast<uint32_t*>(lds_raw + P.pool_off + 8 + 8 * (kBlock / 64));
+  // this wave's reservation: items [res[0], res[1]) claimed and not yet handed out; res[2] = the head
+  // position its last atomic returned (the range's progress, for the chunk guard)
+  long long* res = reinterpret_cast<long long*>(lds_raw + P.pool_off + kResOff) + 3 * (threadIdx.x >> 6);
+  if ((threadIdx.x & 63) < 3) res[threadIdx.x & 63] = 0;
   if (threadIdx.x == 0) {
     *pool_live = kBlock / 64;
     for (int w = 0; w < kBlock / 64; ++w) pool_mask[w] = 0ull;
@@ -805,25 +818,46 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
       const long long g1 = (n_tiles * (head + 1) / kGroups) * 64;
       const int cnt = __popcll(m_fetch);
       const int leader = __ffsll((long long)m_fetch) - 1;
-      if ((*pool_exh >> head) & 1u) {   // another wave of the block found it exhausted
-        head = (head + 1) % kGroups;
-        heads_left--;
-        continue;
+      long long start, limit;   // this pass hands out items [start, limit)
+      const long long rn = res[0], re = res[1];   // (wave-uniform LDS words)
+      if (rn < re) {   // served from the reservation: no atomic
+        start = rn;
+        limit = min(re, rn + cnt);
+        wave_lds_sync();
+        if (lane == leader) res[0] = limit;
+      } else {
+        if ((*pool_exh >> head) & 1u) {   // another wave of the block found it exhausted
+          head = (head + 1) % kGroups;
+          heads_left--;
+          wave_lds_sync();
+          if (lane == leader) res[2] = 1LL << 60;   // other heads near their end: no chunks there
+          continue;
+        }
+        // a chunk while the range is far from its end, else exactly the idle lanes
+        const long long want = (g1 - g0) - res[2] > kChunkGuard ? max((long long)cnt, kChunk) : (long long)cnt;
+        unsigned long long base = 0;
+        if (lane == leader) base = atomicAdd(&P.heads[head * kHeadStride], (unsigned long long)want);
+        base = __shfl(base, leader);
+        start = g0 + (long long)base;
+        if (start >= g1) {   // head exhausted: move to the next XCD group's range
+          wave_lds_sync();
+          if (lane == leader) { atomicOr(pool_exh, 1u << head); res[2] = 1LL << 60; }
+          head = (head + 1) % kGroups;
+          heads_left--;
+          continue;
+        }
+        limit = min(g1, start + cnt);
+        wave_lds_sync();
+        if (lane == leader) {   // the surplus of the chunk (within the range) is kept for later refills
+          res[0] = limit;
+          res[1] = min(g1, start + want);
+          res[2] = (long long)base + want;
+        }
       }
-      unsigned long long base = 0;
-      if (lane == leader) base = atomicAdd(&P.heads[head * kHeadStride], (unsigned long long)cnt);
-      base = __shfl(base, leader);
-      const long long start = g0 + (long long)base;
-      if (start >= g1) {   // head exhausted: move to the next XCD group's range
-        if (lane == leader) atomicOr(pool_exh, 1u << head);
-        head = (head + 1) % kGroups;
-        heads_left--;
-        continue;
-      }
-      if (STATS) { w_refill = __builtin_amdgcn_s_memrealtime(); w_pixels += (unsigned long long)min((long long)cnt, g1 - start); }
+      if (STATS) { w_refill = __builtin_amdgcn_s_memrealtime(); w_pixels += (unsigned long long)(limit - start); }
       if (state == ST_FETCH) {
         const long long wk = start + __popcll(m_fetch & lane_below);
-        if (wk < g1) {
+        if (wk < limit) {
           if (P.list) {   // adaptive pass: one sample of a listed pixel
             const uint32_t id = wk < n_list ? P.list[wk / P.nsamp] : 0xffffffffu;
             const uint32_t pix = id & kListPixMask;
