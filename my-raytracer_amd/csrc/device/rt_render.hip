@@ -639,7 +639,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
     *pool_exh = 0u;
   }
   // once per persistent block: the top treelet and the lights -> LDS
-  if (WIDTH == 4 && P.n_top > 0) {
+  if (WIDTH >= 4 && P.n_top > 0) {
     float4* dst = reinterpret_cast<float4*>(lds_raw + P.top_off);
     const float4* src = reinterpret_cast<const float4*>(P.nodes4);
     for (int i = threadIdx.x; i < P.n_top * (int)(sizeof(GNode4) / sizeof(float4)); i += kBlock) dst[i] = src[i];
@@ -1020,7 +1020,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
         for (int k = 0; k < 3; ++k) {
           float df = (float)d3v[k];
           if (fabsf(df) < 1e-20f) df = signbit(d3v[k]) ? -1e-20f : 1e-20f;
-          if constexpr (WIDTH == 4) {
+          if constexpr (WIDTH >= 4) {
             // v_rcp_f32 (1 ulp) + one Newton step: within about half an ulp of 1 / df, as the
             // correctly rounded division (11 VALU) it replaces; the box error bound of DESIGN.md
             // §4 stays far inside delta.  (The 2-wide canonical kernel keeps the oracle's division.)
@@ -1264,16 +1264,32 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
             tl_it++; wave_tick(tl_wn, tl_dummy, lane);
           }
           if (STATS) { c_nodes++; wave_tick(d_node_it, d_node_ln, lane); wave_distinct(cur, d_node_lines, lane); }
-          float k[4];
-          uint32_t v[4];
+          // WIDTH 8: two 128-B halves (children 0-3 at the node's id, 4-7 at id + 1), same layout each
+          constexpr int NW = WIDTH == 8 ? 8 : 4;
+          float k[NW];
+          uint32_t v[NW];
           int cnt = 0;
+          // wave-uniform: every active lane's node is in the LDS treelet -> ds_read, no TD cost
+          const bool in_lds = wballot(cur >= (uint32_t)P.n_top) == 0;
+          if (STATS) {
+            if (in_lds) {
+              wave_tick(d_node_lds, d_dummy, lane);
+            } else {
+              wave_distinct(cur, d_gn_dist, lane);
+              const uint32_t c0 = __shfl(cur, __ffsll((long long)wballot(1)) - 1);
+              if (wballot(cur != c0) == 0) wave_tick(d_gn_uni, d_dummy, lane);
+            }
+          }
+          if constexpr (TL) {
+            if (in_lds) tl_wave_gap(2);
+            else { tl_gnode++; tl_wave_gap(1); }
+          }
+#pragma unroll
+          for (int hf = 0; hf < NW / 4; ++hf) {
           float4 nx, fx, ny, fy, nz, fz;
           uint4 rf;
-          // wave-uniform: every active lane's node is in the LDS treelet -> ds_read, no TD cost
-          if (wballot(cur >= (uint32_t)P.n_top) == 0) {
-            if (STATS) wave_tick(d_node_lds, d_dummy, lane);
-            if constexpr (TL) tl_wave_gap(2);
-            const unsigned char* lb = lds_raw + P.top_off + cur * (uint32_t)sizeof(GNode4);
+          if (in_lds) {
+            const unsigned char* lb = lds_raw + P.top_off + (cur + (uint32_t)hf) * (uint32_t)sizeof(GNode4);
             nx = *reinterpret_cast<const float4*>(lb + nxo);
             fx = *reinterpret_cast<const float4*>(lb + (nxo ^ 16u));
             ny = *reinterpret_cast<const float4*>(lb + nyo);
@@ -1286,14 +1302,8 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
             // form, one 32-bit OR per plane instead of 64-bit address arithmetic (office +0.7 %,
             // config 4 +1.1 %; the node array stays below 4 GB: checked at upload)
             const char* nbase = reinterpret_cast<const char*>(P.nodes4);
-            const uint32_t nbo = cur * (uint32_t)sizeof(GNode4);
+            const uint32_t nbo = (cur + (uint32_t)hf) * (uint32_t)sizeof(GNode4);
 #define RT_NODE_AT(off) (nbase + (uint32_t)(nbo + (off)))
-            if constexpr (TL) { tl_gnode++; tl_wave_gap(1); }
-            if (STATS) {
-              wave_distinct(cur, d_gn_dist, lane);
-              const uint32_t c0 = __shfl(cur, __ffsll((long long)wballot(1)) - 1);
-              if (wballot(cur != c0) == 0) wave_tick(d_gn_uni, d_dummy, lane);
-            }
             nx = *reinterpret_cast<const float4*>(RT_NODE_AT(nxo));
             fx = *reinterpret_cast<const float4*>(RT_NODE_AT(nxo ^ 16u));
             ny = *reinterpret_cast<const float4*>(RT_NODE_AT(nyo));
@@ -1315,23 +1325,32 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
             const float tf = fminf(fminf(tx1, ty1), __builtin_amdgcn_fmed3f(tz1, hi_c, -pinf));
             const uint32_t r = u4c(rf, c);
             const bool h = tn <= tf;   // absent children carry the empty box [+inf, -inf]
-            k[c] = h ? tn : INFINITY;
-            v[c] = r;
+            k[4 * hf + c] = h ? tn : INFINITY;
+            v[4 * hf + c] = r;
             cnt += h ? 1 : 0;
+          }
           }
 #define RT_CSWAP(a, b)                                        \
   if (k[b] < k[a]) {                                          \
     const float tk = k[a]; k[a] = k[b]; k[b] = tk;            \
     const uint32_t tv = v[a]; v[a] = v[b]; v[b] = tv;         \
   }
-          RT_CSWAP(0, 1) RT_CSWAP(2, 3) RT_CSWAP(0, 2) RT_CSWAP(1, 3) RT_CSWAP(1, 2)
+          if constexpr (NW == 8) {   // Batcher's 19-comparator network
+            RT_CSWAP(0, 1) RT_CSWAP(2, 3) RT_CSWAP(4, 5) RT_CSWAP(6, 7)
+            RT_CSWAP(0, 2) RT_CSWAP(1, 3) RT_CSWAP(4, 6) RT_CSWAP(5, 7)
+            RT_CSWAP(1, 2) RT_CSWAP(5, 6) RT_CSWAP(0, 4) RT_CSWAP(3, 7)
+            RT_CSWAP(1, 5) RT_CSWAP(2, 6) RT_CSWAP(1, 4) RT_CSWAP(3, 6)
+            RT_CSWAP(2, 4) RT_CSWAP(3, 5) RT_CSWAP(3, 4)
+          } else {
+            RT_CSWAP(0, 1) RT_CSWAP(2, 3) RT_CSWAP(0, 2) RT_CSWAP(1, 3) RT_CSWAP(1, 2)
+          }
 #undef RT_CSWAP
           if (cnt == 0) {
             cur = pop();
           } else {
-            if (cnt > 3) push(v[3]);
-            if (cnt > 2) push(v[2]);
-            if (cnt > 1) push(v[1]);
+#pragma unroll
+            for (int c = NW - 1; c >= 1; --c)
+              if (cnt > c) push(v[c]);
             cur = v[0];
           }
           if ((cur & kLeaf) && cur != kDone && pleaf == kDone) {   // first leaf: postpone, keep going
@@ -2062,7 +2081,8 @@ struct Variant {
 // (the traversal the oracle replicates: tests pin its node / triangle counts),
 // [3] production + per-round timeline (RT_FLAG_TIMELINE, diagnostics), [4] production with a
 // 16-entry stack ring (deep hierarchies), [5] the same with suspend/resume traversal (deep
-// hierarchies' several-frame launches).
+// hierarchies' several-frame launches); [6]-[9] the 8-wide counterparts of [0], [4], [5], [1]
+// (rt_upload_options.node_width = 8).
 const Variant kVariants[] = {
     {render_kernel<4, false>, false},
     {render_kernel<4, true>, true},
@@ -2070,10 +2090,15 @@ const Variant kVariants[] = {
     {render_kernel<4, false, true>, false},
     {render_kernel<4, false, false, 16>, false},
     {render_kernel<4, false, false, 16, true>, false},
+    {render_kernel<8, false>, false},
+    {render_kernel<8, false, false, 16>, false},
+    {render_kernel<8, false, false, 16, true>, false},
+    {render_kernel<8, true>, true},
 };
-constexpr int kNumVariants = 6;
+constexpr int kNumVariants = 10;
 constexpr int kRingDeep = 16;
-inline int variant_ring(int v) { return (v == 4 || v == 5) ? kRingDeep : kShortStack; }
+inline int variant_ring(int v) { return (v == 4 || v == 5 || v == 7 || v == 8) ? kRingDeep : kShortStack; }
+inline bool variant_wide8(int v) { return v >= 6; }
 // LDS per block: the variant's stack ring (ring entries per thread, at address 0: the kernel's
 // slot offsets are compile-time constants), kSlotDoubles doubles of slot, task + visibility words.
 size_t lds_bytes(int /*stack_words*/, int ring = kShortStack) {
@@ -2143,6 +2168,7 @@ struct rt_scene {
   int n_cu = 0;
   int blocks_per_cu[kNumVariants] = {};
   bool deep = false;            // launches use the 16-entry ring variant (deep hierarchy)
+  bool wide8 = false;           // 8-wide nodes (rt_upload_options.node_width = 8): the 8-wide variants
   int n_top_v[kNumVariants] = {};   // treelet nodes of each kernel variant (by its stack ring)
   GNode4* d_nodes4 = nullptr;
   int n_gnodes4 = 0;
@@ -2257,6 +2283,7 @@ int upload_image(const SceneImage& I, const rt_upload_options& opt, int device, 
   // deep hierarchies (half a million device records and more: random-triangle soups of ~1 M and
   // up spill an 8-entry ring on every other ray, the office proxy on 1 in 130) render with the
   // 16-entry ring and the 9-node treelet that fits beside it (A/B)
+  sc->wide8 = opt.node_width == 8;
   sc->deep = I.tris.size() >= (size_t)(1u << 18);   // device records (office 77 k prefers 8, 500 k random 16)
   if (opt.stack_ring != 0) sc->deep = opt.stack_ring >= 16;   // forced ring size
   for (int v = 0; v < kNumVariants; ++v) {
@@ -2264,6 +2291,7 @@ int upload_image(const SceneImage& I, const rt_upload_options& opt, int device, 
     nt = top_nodes_for(sc->stack_words, variant_ring(v), sc->n_gnodes4);
     if (opt.lds_treelet > 0) nt = std::min(nt, opt.lds_treelet);   // cache at most this many nodes
     if (opt.lds_treelet < 0) nt = 0;                                // none
+    if (variant_wide8(v)) nt &= ~1;                                  // whole 8-wide nodes (two halves)
   }
   sc->bpc_cap = opt.blocks_per_cu;
   sc->grid_spare = opt.grid_spare;
@@ -2669,13 +2697,17 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
     }
   }
 
-  const int v = (p->flags & RT_FLAG_TRAVERSAL_STATS) ? 2
-                : (p->flags & RT_FLAG_WIDE_STATS) ? 1
-                : (p->flags & RT_FLAG_TIMELINE) ? 3
-                // 4/5: the 16-entry-ring production variants; suspend/resume on deep scenes' several-
-                // frame launches (config 4, 128 frames: +3.2 %; one frame: -6 %, so not there)
-                : sc->deep ? ((n_frames > 1 && !list) ? 5 : 4)
-                : 0;
+  int v = (p->flags & RT_FLAG_TRAVERSAL_STATS) ? 2
+          : (p->flags & RT_FLAG_WIDE_STATS) ? 1
+          : (p->flags & RT_FLAG_TIMELINE) ? 3
+          // 4/5: the 16-entry-ring production variants; suspend/resume on deep scenes' several-
+          // frame launches (config 4, 128 frames: +3.2 %; one frame: -6 %, so not there)
+          : sc->deep ? ((n_frames > 1 && !list) ? 5 : 4)
+          : 0;
+  if (sc->wide8 && v != 2) {   // the scene's nodes are 8-wide: the 8-wide counterpart
+    if (v == 3) return fail(RT_ERR_UNSUPPORTED, "rt_launch: the round timeline needs 4-wide nodes");
+    v = v == 0 ? 6 : v == 4 ? 7 : v == 5 ? 8 : 9;
+  }
   const int ring = variant_ring(v);
   const int n_top = sc->n_top_v[v];
   const size_t lds = lds_bytes_total(sc->stack_words, n_top, ring);

@@ -1,5 +1,6 @@
 """Interleaved A/B of kernel libraries on single-frame and batched frame time (dev tool, under
-gpurun).  usage: python tools/ab_frame.py ROUNDS lib1 lib2 ... [-- scene [tris]]"""
+gpurun).  usage: python tools/ab_frame.py ROUNDS lib1 lib2 ... [-- scene [tris]]
+A library entry may carry upload options after '#': lib.so#node_width=8,stack_ring=16."""
 import json
 import os
 import subprocess
@@ -16,7 +17,8 @@ R, libs = int(args[0]), args[1:]
 res = {l: [] for l in libs}
 for r in range(R):
     for l in libs:
-        env = dict(os.environ, RTAMD_HIP_LIB=os.path.abspath(l))
+        path, _, opts = l.partition("#")
+        env = dict(os.environ, RTAMD_HIP_LIB=os.path.abspath(path), RTAMD_AB_OPTS=opts)
         o = subprocess.run([sys.executable, "tools/frame_probe.py", *extra], env=env, capture_output=True,
                            text=True, timeout=300)
         if o.returncode != 0:
@@ -28,4 +30,4 @@ for r in range(R):
 for l, v in res.items():
     s = np.median([d["single_ms"] for d in v])
     b = np.median([d["batched_ms_per_frame"] for d in v])
-    print(f"{os.path.basename(l):32s} single {s:.4f} ms   batched {b:.4f} ms/frame", flush=True)
+    print(f"{os.path.basename(l):48s} single {s:.4f} ms   batched {b:.4f} ms/frame", flush=True)

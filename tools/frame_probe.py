@@ -1,7 +1,8 @@
 """One kernel library, office 1080p (dev tool, under gpurun; run by tools/ab_frame.py with
 RTAMD_HIP_LIB set): median kernel time of single-frame launches and of 64-frame launches
-(per frame), printed as one JSON line."""
+(per frame), printed as one JSON line.  RTAMD_AB_OPTS: upload options "key=value,..."."""
 import json
+import os
 import sys
 
 import numpy as np
@@ -14,7 +15,8 @@ scene = sys.argv[1] if len(sys.argv) > 1 else "office"
 gen = {"n_triangles": int(sys.argv[2])} if len(sys.argv) > 2 else {}
 host = rtamd.HostScene.generate(scene, **gen)
 host.prepare()
-gpu = rtamd.DeviceScene(host, 0)
+opts = dict(kv.split("=") for kv in os.environ.get("RTAMD_AB_OPTS", "").split(",") if kv)
+gpu = rtamd.DeviceScene(host, 0, **{k: int(v) for k, v in opts.items()})
 p = host.render_params(1920, 1080, 1)
 out = [torch.zeros((1080, 1920, 3), device="cuda") for _ in range(64)]
 for _ in range(5):
