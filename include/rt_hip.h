@@ -222,9 +222,7 @@ typedef struct rt_upload_options {
                             (32 = one XCD's worth: the smallest reservation a 256-VGPR kernel was
                             measured to run beside); 0 = none (default; rt_multi_create: 32 per GPU at
                             N > 1); -1 = none */
-  int node_width;        /* children per traversal node: 0 or 4 = 4-wide (default), 8 = 8-wide (two 128-B
-                            halves per node: fewer, wider dependent iterations on deep hierarchies) */
-  int reserved_[6];
+  int reserved_[7];
 } rt_upload_options;
 
 /* Fills *opt with the defaults listed above. */

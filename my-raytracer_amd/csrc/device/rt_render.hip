@@ -72,20 +72,9 @@ constexpr int kShortStack = 8;
 // into each block's LDS; a node iteration whose active lanes all sit in the treelet reads
 // LDS instead of the vector-L1 path.  0 disables.
 // LDS per thread: kSlotDoubles fp64 slot words, task + visibility words, the stack ring
-// LDS pool: live-wave count, one 64-bit lane mask per wave of the block, exhausted heads; then per
-// wave its work reservation {next, end, head position last seen} (3 u64)
-constexpr int kResOff = 48;
-constexpr int kPoolBytes = kResOff + 24 * (kBlock / 64);
-static_assert(8 + 8 * (kBlock / 64) + 4 <= kResOff, "compaction pool does not fit");
-// Work reservations: a refilling wave claims kChunk work items from its head with one device atomic
-// while the head's range has more than kChunkGuard items left, keeps the surplus in its LDS words
-// and serves later refills from them (no atomic); near a range's end it claims exactly what it needs
-// (the surplus of 512 waves per head would otherwise leave some waves a tile or two behind at the end)
-constexpr long long kChunk = 128;
-constexpr long long kChunkGuard = 2 * 512 * kChunk;
 constexpr int kSlotDoubles = 10;
-// fills the CU's 160 KB at 4 blocks with the slots, ring, lights, pool (72 nodes)
-constexpr int kTopNodes = (40960 - kBlock * (kSlotDoubles * 8 + (2 + kShortStack) * 4) - RT_MAX_LIGHTS * 48 - kPoolBytes) / 128;
+// fills the CU's 160 KB at 4 blocks with the slots, ring, lights, pool (73 nodes)
+constexpr int kTopNodes = (40960 - kBlock * (kSlotDoubles * 8 + (2 + kShortStack) * 4) - RT_MAX_LIGHTS * 48 - 64) / 128;
 constexpr int kStackMask = kShortStack - 1;
 // Tail compaction: once the work queue is empty, a wave with at most kDonateMax
 // pixels in flight hands them to the other waves of its block and exits, so the last pixels
@@ -95,6 +84,8 @@ constexpr int kStackMask = kShortStack - 1;
 constexpr int kDonateMax = 24;   // (0 = tail compaction off: -2.8 % batched, -1.4 % one frame)
 constexpr int kMigWords = 8;
 static_assert(kMigWords <= kShortStack, "migration words travel in the stack ring entries");
+constexpr int kPoolBytes = 64;   // LDS: live-wave count, one 64-bit lane mask per wave of the block, exhausted heads
+static_assert(8 + 8 * (kBlock / 64) + 4 <= kPoolBytes, "compaction pool does not fit");
 static_assert((kShortStack & kStackMask) == 0, "the stack ring must be a power of two");
 
 // Lane states.  Owners carry a pixel (CLOSEST: closest-hit ray in flight; SHADOW: a
@@ -629,17 +620,13 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
   unsigned long long* pool_mask = reinterpret_cast<unsigned long long*>(lds_raw + P.pool_off + 8);
   // heads this block found exhausted (skipped without an atomic)
   uint32_t* pool_exh = reinterpret_cast<uint32_t*>(lds_raw + P.pool_off + 8 + 8 * (kBlock / 64));
-  // this wave's reservation: items [res[0], res[1]) claimed and not yet handed out; res[2] = the head
-  // position its last atomic returned (the range's progress, for the chunk guard)
-  long long* res = reinterpret_cast<long long*>(lds_raw + P.pool_off + kResOff) + 3 * (threadIdx.x >> 6);
-  if ((threadIdx.x & 63) < 3) res[threadIdx.x & 63] = 0;
   if (threadIdx.x == 0) {
     *pool_live = kBlock / 64;
     for (int w = 0; w < kBlock / 64; ++w) pool_mask[w] = 0ull;
     *pool_exh = 0u;
   }
   // once per persistent block: the top treelet and the lights -> LDS
-  if (WIDTH >= 4 && P.n_top > 0) {
+  if (WIDTH == 4 && P.n_top > 0) {
     float4* dst = reinterpret_cast<float4*>(lds_raw + P.top_off);
     const float4* src = reinterpret_cast<const float4*>(P.nodes4);
     for (int i = threadIdx.x; i < P.n_top * (int)(sizeof(GNode4) / sizeof(float4)); i += kBlock) dst[i] = src[i];
@@ -818,46 +805,25 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
       const long long g1 = (n_tiles * (head + 1) / kGroups) * 64;
       const int cnt = __popcll(m_fetch);
       const int leader = __ffsll((long long)m_fetch) - 1;
-      long long start, limit;   // this pass hands out items [start, limit)
-      const long long rn = res[0], re = res[1];   // (wave-uniform LDS words)
-      if (rn < re) {   // served from the reservation: no atomic
-        start = rn;
-        limit = min(re, rn + cnt);
-        wave_lds_sync();
-        if (lane == leader) res[0] = limit;
-      } else {
-        if ((*pool_exh >> head) & 1u) {   // another wave of the block found it exhausted
-          head = (head + 1) % kGroups;
-          heads_left--;
-          wave_lds_sync();
-          if (lane == leader) res[2] = 1LL << 60;   // other heads near their end: no chunks there
-          continue;
-        }
-        // a chunk while the range is far from its end, else exactly the idle lanes
-        const long long want = (g1 - g0) - res[2] > kChunkGuard ? max((long long)cnt, kChunk) : (long long)cnt;
-        unsigned long long base = 0;
-        if (lane == leader) base = atomicAdd(&P.heads[head * kHeadStride], (unsigned long long)want);
-        base = __shfl(base, leader);
-        start = g0 + (long long)base;
-        if (start >= g1) {   // head exhausted: move to the next XCD group's range
-          wave_lds_sync();
-          if (lane == leader) { atomicOr(pool_exh, 1u << head); res[2] = 1LL << 60; }
-          head = (head + 1) % kGroups;
-          heads_left--;
-          continue;
-        }
-        limit = min(g1, start + cnt);
-        wave_lds_sync();
-        if (lane == leader) {   // the surplus of the chunk (within the range) is kept for later refills
-          res[0] = limit;
-          res[1] = min(g1, start + want);
-          res[2] = (long long)base + want;
-        }
+      if ((*pool_exh >> head) & 1u) {   // another wave of the block found it exhausted
+        head = (head + 1) % kGroups;
+        heads_left--;
+        continue;
       }
-      if (STATS) { w_refill = __builtin_amdgcn_s_memrealtime(); w_pixels += (unsigned long long)(limit - start); }
+      unsigned long long base = 0;
+      if (lane == leader) base = atomicAdd(&P.heads[head * kHeadStride], (unsigned long long)cnt);
+      base = __shfl(base, leader);
+      const long long start = g0 + (long long)base;
+      if (start >= g1) {   // head exhausted: move to the next XCD group's range
+        if (lane == leader) atomicOr(pool_exh, 1u << head);
+        head = (head + 1) % kGroups;
+        heads_left--;
+        continue;
+      }
+      if (STATS) { w_refill = __builtin_amdgcn_s_memrealtime(); w_pixels += (unsigned long long)min((long long)cnt, g1 - start); }
       if (state == ST_FETCH) {
         const long long wk = start + __popcll(m_fetch & lane_below);
-        if (wk < limit) {
+        if (wk < g1) {
           if (P.list) {   // adaptive pass: one sample of a listed pixel
             const uint32_t id = wk < n_list ? P.list[wk / P.nsamp] : 0xffffffffu;
             const uint32_t pix = id & kListPixMask;
@@ -1020,7 +986,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
         for (int k = 0; k < 3; ++k) {
           float df = (float)d3v[k];
           if (fabsf(df) < 1e-20f) df = signbit(d3v[k]) ? -1e-20f : 1e-20f;
-          if constexpr (WIDTH >= 4) {
+          if constexpr (WIDTH == 4) {
             // v_rcp_f32 (1 ulp) + one Newton step: within about half an ulp of 1 / df, as the
             // correctly rounded division (11 VALU) it replaces; the box error bound of DESIGN.md
             // §4 stays far inside delta.  (The 2-wide canonical kernel keeps the oracle's division.)
@@ -1264,32 +1230,16 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
             tl_it++; wave_tick(tl_wn, tl_dummy, lane);
           }
           if (STATS) { c_nodes++; wave_tick(d_node_it, d_node_ln, lane); wave_distinct(cur, d_node_lines, lane); }
-          // WIDTH 8: two 128-B halves (children 0-3 at the node's id, 4-7 at id + 1), same layout each
-          constexpr int NW = WIDTH == 8 ? 8 : 4;
-          float k[NW];
-          uint32_t v[NW];
+          float k[4];
+          uint32_t v[4];
           int cnt = 0;
-          // wave-uniform: every active lane's node is in the LDS treelet -> ds_read, no TD cost
-          const bool in_lds = wballot(cur >= (uint32_t)P.n_top) == 0;
-          if (STATS) {
-            if (in_lds) {
-              wave_tick(d_node_lds, d_dummy, lane);
-            } else {
-              wave_distinct(cur, d_gn_dist, lane);
-              const uint32_t c0 = __shfl(cur, __ffsll((long long)wballot(1)) - 1);
-              if (wballot(cur != c0) == 0) wave_tick(d_gn_uni, d_dummy, lane);
-            }
-          }
-          if constexpr (TL) {
-            if (in_lds) tl_wave_gap(2);
-            else { tl_gnode++; tl_wave_gap(1); }
-          }
-#pragma unroll
-          for (int hf = 0; hf < NW / 4; ++hf) {
           float4 nx, fx, ny, fy, nz, fz;
           uint4 rf;
-          if (in_lds) {
-            const unsigned char* lb = lds_raw + P.top_off + (cur + (uint32_t)hf) * (uint32_t)sizeof(GNode4);
+          // wave-uniform: every active lane's node is in the LDS treelet -> ds_read, no TD cost
+          if (wballot(cur >= (uint32_t)P.n_top) == 0) {
+            if (STATS) wave_tick(d_node_lds, d_dummy, lane);
+            if constexpr (TL) tl_wave_gap(2);
+            const unsigned char* lb = lds_raw + P.top_off + cur * (uint32_t)sizeof(GNode4);
             nx = *reinterpret_cast<const float4*>(lb + nxo);
             fx = *reinterpret_cast<const float4*>(lb + (nxo ^ 16u));
             ny = *reinterpret_cast<const float4*>(lb + nyo);
@@ -1302,8 +1252,14 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
             // form, one 32-bit OR per plane instead of 64-bit address arithmetic (office +0.7 %,
             // config 4 +1.1 %; the node array stays below 4 GB: checked at upload)
             const char* nbase = reinterpret_cast<const char*>(P.nodes4);
-            const uint32_t nbo = (cur + (uint32_t)hf) * (uint32_t)sizeof(GNode4);
+            const uint32_t nbo = cur * (uint32_t)sizeof(GNode4);
 #define RT_NODE_AT(off) (nbase + (uint32_t)(nbo + (off)))
+            if constexpr (TL) { tl_gnode++; tl_wave_gap(1); }
+            if (STATS) {
+              wave_distinct(cur, d_gn_dist, lane);
+              const uint32_t c0 = __shfl(cur, __ffsll((long long)wballot(1)) - 1);
+              if (wballot(cur != c0) == 0) wave_tick(d_gn_uni, d_dummy, lane);
+            }
             nx = *reinterpret_cast<const float4*>(RT_NODE_AT(nxo));
             fx = *reinterpret_cast<const float4*>(RT_NODE_AT(nxo ^ 16u));
             ny = *reinterpret_cast<const float4*>(RT_NODE_AT(nyo));
@@ -1325,32 +1281,23 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
             const float tf = fminf(fminf(tx1, ty1), __builtin_amdgcn_fmed3f(tz1, hi_c, -pinf));
             const uint32_t r = u4c(rf, c);
             const bool h = tn <= tf;   // absent children carry the empty box [+inf, -inf]
-            k[4 * hf + c] = h ? tn : INFINITY;
-            v[4 * hf + c] = r;
+            k[c] = h ? tn : INFINITY;
+            v[c] = r;
             cnt += h ? 1 : 0;
-          }
           }
 #define RT_CSWAP(a, b)                                        \
   if (k[b] < k[a]) {                                          \
     const float tk = k[a]; k[a] = k[b]; k[b] = tk;            \
     const uint32_t tv = v[a]; v[a] = v[b]; v[b] = tv;         \
   }
-          if constexpr (NW == 8) {   // Batcher's 19-comparator network
-            RT_CSWAP(0, 1) RT_CSWAP(2, 3) RT_CSWAP(4, 5) RT_CSWAP(6, 7)
-            RT_CSWAP(0, 2) RT_CSWAP(1, 3) RT_CSWAP(4, 6) RT_CSWAP(5, 7)
-            RT_CSWAP(1, 2) RT_CSWAP(5, 6) RT_CSWAP(0, 4) RT_CSWAP(3, 7)
-            RT_CSWAP(1, 5) RT_CSWAP(2, 6) RT_CSWAP(1, 4) RT_CSWAP(3, 6)
-            RT_CSWAP(2, 4) RT_CSWAP(3, 5) RT_CSWAP(3, 4)
-          } else {
-            RT_CSWAP(0, 1) RT_CSWAP(2, 3) RT_CSWAP(0, 2) RT_CSWAP(1, 3) RT_CSWAP(1, 2)
-          }
+          RT_CSWAP(0, 1) RT_CSWAP(2, 3) RT_CSWAP(0, 2) RT_CSWAP(1, 3) RT_CSWAP(1, 2)
 #undef RT_CSWAP
           if (cnt == 0) {
             cur = pop();
           } else {
-#pragma unroll
-            for (int c = NW - 1; c >= 1; --c)
-              if (cnt > c) push(v[c]);
+            if (cnt > 3) push(v[3]);
+            if (cnt > 2) push(v[2]);
+            if (cnt > 1) push(v[1]);
             cur = v[0];
           }
           if ((cur & kLeaf) && cur != kDone && pleaf == kDone) {   // first leaf: postpone, keep going
@@ -2081,8 +2028,7 @@ struct Variant {
 // (the traversal the oracle replicates: tests pin its node / triangle counts),
 // [3] production + per-round timeline (RT_FLAG_TIMELINE, diagnostics), [4] production with a
 // 16-entry stack ring (deep hierarchies), [5] the same with suspend/resume traversal (deep
-// hierarchies' several-frame launches); [6]-[9] the 8-wide counterparts of [0], [4], [5], [1]
-// (rt_upload_options.node_width = 8).
+// hierarchies' several-frame launches).
 const Variant kVariants[] = {
     {render_kernel<4, false>, false},
     {render_kernel<4, true>, true},
@@ -2090,15 +2036,10 @@ const Variant kVariants[] = {
     {render_kernel<4, false, true>, false},
     {render_kernel<4, false, false, 16>, false},
     {render_kernel<4, false, false, 16, true>, false},
-    {render_kernel<8, false>, false},
-    {render_kernel<8, false, false, 16>, false},
-    {render_kernel<8, false, false, 16, true>, false},
-    {render_kernel<8, true>, true},
 };
-constexpr int kNumVariants = 10;
+constexpr int kNumVariants = 6;
 constexpr int kRingDeep = 16;
-inline int variant_ring(int v) { return (v == 4 || v == 5 || v == 7 || v == 8) ? kRingDeep : kShortStack; }
-inline bool variant_wide8(int v) { return v >= 6; }
+inline int variant_ring(int v) { return (v == 4 || v == 5) ? kRingDeep : kShortStack; }
 // LDS per block: the variant's stack ring (ring entries per thread, at address 0: the kernel's
 // slot offsets are compile-time constants), kSlotDoubles doubles of slot, task + visibility words.
 size_t lds_bytes(int /*stack_words*/, int ring = kShortStack) {
@@ -2168,7 +2109,6 @@ struct rt_scene {
   int n_cu = 0;
   int blocks_per_cu[kNumVariants] = {};
   bool deep = false;            // launches use the 16-entry ring variant (deep hierarchy)
-  bool wide8 = false;           // 8-wide nodes (rt_upload_options.node_width = 8): the 8-wide variants
   int n_top_v[kNumVariants] = {};   // treelet nodes of each kernel variant (by its stack ring)
   GNode4* d_nodes4 = nullptr;
   int n_gnodes4 = 0;
@@ -2283,7 +2223,6 @@ int upload_image(const SceneImage& I, const rt_upload_options& opt, int device, 
   // deep hierarchies (half a million device records and more: random-triangle soups of ~1 M and
   // up spill an 8-entry ring on every other ray, the office proxy on 1 in 130) render with the
   // 16-entry ring and the 9-node treelet that fits beside it (A/B)
-  sc->wide8 = opt.node_width == 8;
   sc->deep = I.tris.size() >= (size_t)(1u << 18);   // device records (office 77 k prefers 8, 500 k random 16)
   if (opt.stack_ring != 0) sc->deep = opt.stack_ring >= 16;   // forced ring size
   for (int v = 0; v < kNumVariants; ++v) {
@@ -2291,7 +2230,6 @@ int upload_image(const SceneImage& I, const rt_upload_options& opt, int device, 
     nt = top_nodes_for(sc->stack_words, variant_ring(v), sc->n_gnodes4);
     if (opt.lds_treelet > 0) nt = std::min(nt, opt.lds_treelet);   // cache at most this many nodes
     if (opt.lds_treelet < 0) nt = 0;                                // none
-    if (variant_wide8(v)) nt &= ~1;                                  // whole 8-wide nodes (two halves)
   }
   sc->bpc_cap = opt.blocks_per_cu;
   sc->grid_spare = opt.grid_spare;
@@ -2697,17 +2635,13 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
     }
   }
 
-  int v = (p->flags & RT_FLAG_TRAVERSAL_STATS) ? 2
-          : (p->flags & RT_FLAG_WIDE_STATS) ? 1
-          : (p->flags & RT_FLAG_TIMELINE) ? 3
-          // 4/5: the 16-entry-ring production variants; suspend/resume on deep scenes' several-
-          // frame launches (config 4, 128 frames: +3.2 %; one frame: -6 %, so not there)
-          : sc->deep ? ((n_frames > 1 && !list) ? 5 : 4)
-          : 0;
-  if (sc->wide8 && v != 2) {   // the scene's nodes are 8-wide: the 8-wide counterpart
-    if (v == 3) return fail(RT_ERR_UNSUPPORTED, "rt_launch: the round timeline needs 4-wide nodes");
-    v = v == 0 ? 6 : v == 4 ? 7 : v == 5 ? 8 : 9;
-  }
+  const int v = (p->flags & RT_FLAG_TRAVERSAL_STATS) ? 2
+                : (p->flags & RT_FLAG_WIDE_STATS) ? 1
+                : (p->flags & RT_FLAG_TIMELINE) ? 3
+                // 4/5: the 16-entry-ring production variants; suspend/resume on deep scenes' several-
+                // frame launches (config 4, 128 frames: +3.2 %; one frame: -6 %, so not there)
+                : sc->deep ? ((n_frames > 1 && !list) ? 5 : 4)
+                : 0;
   const int ring = variant_ring(v);
   const int n_top = sc->n_top_v[v];
   const size_t lds = lds_bytes_total(sc->stack_words, n_top, ring);

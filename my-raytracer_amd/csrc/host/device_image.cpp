@@ -916,8 +916,6 @@ int build_image(const rt_scene_soa* s, const rt_bvh_soa* b, const rt_upload_opti
   if (opt.collapse != RT_COLLAPSE_GREEDY && opt.collapse != RT_COLLAPSE_SAH)
     return fail(RT_ERR_INVALID, "rt_scene_upload: unknown collapse");
   if (opt.build_threads < 0) return fail(RT_ERR_INVALID, "rt_scene_upload: build_threads < 0");
-  if (opt.node_width != 0 && opt.node_width != 4 && opt.node_width != 8)
-    return fail(RT_ERR_INVALID, "rt_scene_upload: node_width must be 0, 4 or 8");
   g_threads = opt.build_threads > 0 ? std::min(opt.build_threads, 64) : std::max(1, std::min(usable_cpus(), 64));
   g_verbose = opt.verbose != 0;
   const bool timing = g_verbose;   // phase times to stderr (diagnostics)
@@ -1011,11 +1009,7 @@ int build_image(const rt_scene_soa* s, const rt_bvh_soa* b, const rt_upload_opti
   std::vector<uint32_t> slot2dev((size_t)std::max<long long>(nt, 1), 0);
   for (long long g = nrec - 1; g >= 0; --g) slot2dev[dev2slot[g]] = (uint32_t)g;
 
-  // ---- 4-wide (or 8-wide) collapse of the device tree (production layout) ----
-  // An 8-wide node is two consecutive GNode4 halves (children 0-3, 4-7); node ids count GNode4
-  // units either way, so an 8-wide node's id is even and its halves sit at id and id + 1.
-  const int W = opt.node_width == 8 ? 8 : 4;
-  const int H = W / 4;   // GNode4 halves per node
+  // ---- 4-wide collapse of the device tree (production layout) ----
   std::vector<GNode4> nodes4;
   int stack4 = 1;
   if (nt > 0) {
@@ -1024,7 +1018,7 @@ int build_image(const rt_scene_soa* s, const rt_bvh_soa* b, const rt_upload_opti
       return dx * dy + dy * dz + dz * dx;
     };
     auto internal = [&](int c) { return E.count[c] == 0; };
-    struct Kids { int c[8]; int n; };
+    struct Kids { int c[4]; int n; };
     // Optional SAH-optimal collapse (RT_COLLAPSE_SAH): D[n][j] = the least SAH cost of covering
     // binary subtree n with at most j child slots; a slot costs area * c_tri for a leaf and
     // area * c_node + D(children, 4) for a wide node (the 4 box tests of a visit are charged to
@@ -1032,46 +1026,46 @@ int build_image(const rt_scene_soa* s, const rt_bvh_soa* b, const rt_upload_opti
     // sweep fills the table.
     const bool dp = opt.collapse == RT_COLLAPSE_SAH;
     const double c_tri = opt.collapse_c_tri;
-    std::vector<std::array<double, 9>> D;
-    std::vector<std::array<int8_t, 9>> Dk;   // 0: n itself is the slot, k > 0: k slots to the left child
+    std::vector<std::array<double, 5>> D;
+    std::vector<std::array<int8_t, 5>> Dk;   // 0: n itself is the slot, k > 0: k slots to the left child
     std::vector<int8_t> Ik;                  // wide node n: slots given to its left child
     if (dp) {
       const size_t nn = E.left.size();
-      D.assign(nn, {});
-      Dk.assign(nn, {});
+      D.assign(nn, {0, 0, 0, 0, 0});
+      Dk.assign(nn, {0, 0, 0, 0, 0});
       Ik.assign(nn, 0);
       for (long long n = (long long)nn - 1; n >= 0; --n) {
         if (!internal((int)n)) {
-          for (int j = 1; j <= W; ++j) D[n][j] = area((int)n) * c_tri;
+          for (int j = 1; j <= 4; ++j) D[n][j] = area((int)n) * c_tri;
           continue;
         }
         const int l = E.left[n], r = E.right[n];
         double best = DBL_MAX;
-        for (int k = 1; k < W; ++k)
-          if (D[l][k] + D[r][W - k] < best) { best = D[l][k] + D[r][W - k]; Ik[n] = (int8_t)k; }
+        for (int k = 1; k <= 3; ++k)
+          if (D[l][k] + D[r][4 - k] < best) { best = D[l][k] + D[r][4 - k]; Ik[n] = (int8_t)k; }
         const double self = area((int)n) + best;   // c_node = 1
         D[n][1] = self;
-        for (int j = 2; j <= W; ++j) {
+        for (int j = 2; j <= 4; ++j) {
           D[n][j] = self;
           for (int k = 1; k < j; ++k)
             if (D[l][k] + D[r][j - k] < D[n][j]) { D[n][j] = D[l][k] + D[r][j - k]; Dk[n][j] = (int8_t)k; }
         }
       }
     }
-    auto kids_of = [&](int n) {   // open the largest internal child until W children
+    auto kids_of = [&](int n) {   // open the largest internal child until 4 children
       if (dp) {
-        Kids k{{-1, -1, -1, -1, -1, -1, -1, -1}, 0};
+        Kids k{{-1, -1, -1, -1}, 0};
         auto expand = [&](auto&& self, int m, int j) -> void {
           if (!internal(m) || Dk[m][j] == 0) { k.c[k.n++] = m; return; }
           self(self, E.left[m], Dk[m][j]);
           self(self, E.right[m], j - Dk[m][j]);
         };
         expand(expand, E.left[n], Ik[n]);
-        expand(expand, E.right[n], W - Ik[n]);
+        expand(expand, E.right[n], 4 - Ik[n]);
         return k;
       }
-      Kids k{{E.left[n], E.right[n], -1, -1, -1, -1, -1, -1}, 2};
-      while (k.n < W) {
+      Kids k{{E.left[n], E.right[n], -1, -1}, 2};
+      while (k.n < 4) {
         int pick = -1;
         double best_a = -1.0;
         for (int i = 0; i < k.n; ++i)
@@ -1101,16 +1095,12 @@ int build_image(const rt_scene_soa* s, const rt_bvh_soa* b, const rt_upload_opti
       g.ref[s_] = kEmpty;
     };
     if (!internal(0)) {
-      for (int h = 0; h < H; ++h) {
-        GNode4 g;
-        std::memset(&g, 0, sizeof g);
-        for (int s_ = 0; s_ < 4; ++s_) set_empty(g, s_);
-        if (h == 0) {
-          set4(g, 0, 0);
-          g.ref[0] = kLeaf | (uint32_t)E.first[0];
-        }
-        nodes4.push_back(g);
-      }
+      GNode4 g;
+      std::memset(&g, 0, sizeof g);
+      set4(g, 0, 0);
+      g.ref[0] = kLeaf | (uint32_t)E.first[0];
+      for (int s_ = 1; s_ < 4; ++s_) set_empty(g, s_);
+      nodes4.push_back(g);
     } else {
       // Numbering: the first bfs_top collapsed nodes in breadth-first order (the top
       // treelet each block caches in LDS), the rest in preorder so a
@@ -1119,15 +1109,14 @@ int build_image(const rt_scene_soa* s, const rt_bvh_soa* b, const rt_upload_opti
       std::vector<Kids> kids;
       std::vector<int> g4(E.left.size(), -1);
       auto assign = [&](int n) {
-        g4[n] = (int)order.size() * H;
+        g4[n] = (int)order.size();
         order.push_back(n);
         kids.push_back(kids_of(n));
       };
       assign(0);
-      const int top_w = bfs_top / H;   // bfs_top counts GNode4 units
-      for (size_t q = 0; q < order.size() && (int)order.size() < top_w; ++q) {   // breadth-first top
+      for (size_t q = 0; q < order.size() && (int)order.size() < bfs_top; ++q) {   // breadth-first top
         const Kids k = kids[q];
-        for (int i = 0; i < k.n && (int)order.size() < top_w; ++i)
+        for (int i = 0; i < k.n && (int)order.size() < bfs_top; ++i)
           if (internal(k.c[i])) assign(k.c[i]);
       }
       std::vector<int> stk;                    // preorder below the treelet
@@ -1145,24 +1134,21 @@ int build_image(const rt_scene_soa* s, const rt_bvh_soa* b, const rt_upload_opti
             if (internal(kn.c[i])) stk.push_back(kn.c[i]);
         }
       }
-      nodes4.resize(order.size() * H);
+      nodes4.resize(order.size());
       std::vector<int> need(order.size(), 0);   // stack entries needed below each node
       for (int gi = (int)order.size() - 1; gi >= 0; --gi) {
+        GNode4& g = nodes4[gi];
+        std::memset(&g, 0, sizeof g);
         const Kids& k = kids[gi];
         int deeper = 0;
-        for (int h = 0; h < H; ++h) {
-          GNode4& g = nodes4[(size_t)gi * H + h];
-          std::memset(&g, 0, sizeof g);
-          for (int q = 0; q < 4; ++q) {
-            const int s_ = 4 * h + q;
-            if (s_ < k.n) {
-              const int c = k.c[s_];
-              set4(g, q, c);
-              g.ref[q] = internal(c) ? (uint32_t)g4[c] : (kLeaf | (uint32_t)E.first[c]);
-              if (internal(c)) deeper = std::max(deeper, need[g4[c] / H]);
-            } else {
-              set_empty(g, q);
-            }
+        for (int s_ = 0; s_ < 4; ++s_) {
+          if (s_ < k.n) {
+            const int c = k.c[s_];
+            set4(g, s_, c);
+            g.ref[s_] = internal(c) ? (uint32_t)g4[c] : (kLeaf | (uint32_t)E.first[c]);
+            if (internal(c)) deeper = std::max(deeper, need[g4[c]]);
+          } else {
+            set_empty(g, s_);
           }
         }
         need[gi] = k.n - 1 + deeper;

@@ -800,38 +800,6 @@ def test_device_tree_changes_no_pixel(kind, kw, w, h, spp):
           f"sbvh {wc.node_visits} / {wc.tri_tests}  reference {wb.node_visits} / {wb.tri_tests}")
 
 
-@pytest.mark.parametrize("kind,kw,w,h,spp,collapse", [
-    ("office", {}, 320, 180, 1, None), ("cornell", {"detail": 3}, 97, 61, 2, None),
-    ("random_tris", {"n_triangles": 20000}, 160, 90, 1, rtamd.abi.RT_COLLAPSE_SAH),
-    ("random_tris", {"n_triangles": 400000}, 160, 90, 1, None)])
-def test_node_width_8_changes_no_pixel(kind, kw, w, h, spp, collapse):
-    # 8-wide nodes (two 128-B halves) visit a different hierarchy in a different order; the
-    # closest hit is the smallest (t, slot) over a conservative superset, so the bits stay.
-    import torch
-
-    hs, four, _ = Case.get(kind, **kw)
-    extra = {} if collapse is None else {"collapse": collapse}
-    eight = rtamd.DeviceScene(hs, 0, node_width=8, **extra)
-    p = hs.render_params(w, h, spp)
-    p.out_format = rtamd.RT_OUT_RGB_F64
-    a, sa = four.render(p)
-    b, sb = eight.render(p)
-    assert np.array_equal(a, b) and counts(sa) == counts(sb)
-    frames = [rtamd.camera_orbit(p, 0.05 * f) for f in range(3)]
-    ref = [four.render(q)[0] for q in frames]
-    outs = [torch.zeros((h, w, 3), dtype=torch.float64, device="cuda") for _ in frames]
-    eight.launch_frames(frames, [o.data_ptr() for o in outs])
-    torch.cuda.synchronize()
-    for r, o in zip(ref, outs):
-        assert np.array_equal(r, o.cpu().numpy())
-    p.flags = rtamd.RT_FLAG_WIDE_STATS
-    _, w4 = four.render(p)
-    _, w8 = eight.render(p)
-    assert w8.node_visits < w4.node_visits   # the point of the option
-    print(f"{kind}: node visits 4-wide {w4.node_visits} 8-wide {w8.node_visits}, tri tests {w4.tri_tests} / {w8.tri_tests}")
-    eight.close()
-
-
 @pytest.mark.parametrize("tree", ["sah", "sbvh"])
 def test_tree_independent_of_build_threads(tree):
     hs = rtamd.HostScene.generate("random_tris", n_triangles=300000, seed=5)
