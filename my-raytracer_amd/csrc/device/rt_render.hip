@@ -60,6 +60,9 @@ using namespace rtk;
 
 namespace {
 
+#ifndef RT_SHADOW_ORDER
+#define RT_SHADOW_ORDER 0   // A/B: 1 = waves of any-hit rays visit children in node order (no sort)
+#endif
 constexpr int kBlock = 256;        // threads per persistent block
 constexpr int kGroups = 8;          // work heads (XCD groups)
 constexpr int kRefill = 16;         // refill a wave when this many lanes are idle (8 / 32: +-0.2 %)
@@ -1165,6 +1168,9 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
       }
 
       uint32_t rounds = 0;
+#if RT_SHADOW_ORDER
+      const bool w_any = wballot(!anyhit && cur != kDone) == 0;   // wave-uniform
+#endif
       while ((wballot(cur != kDone) | wballot(pleaf != kDone)) != 0) {
         if (++rounds > kTravGuard) {   // watchdog: abandon the round (results void, launch flagged)
           guard_trip();
@@ -1290,8 +1296,20 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
     const float tk = k[a]; k[a] = k[b]; k[b] = tk;            \
     const uint32_t tv = v[a]; v[a] = v[b]; v[b] = tv;         \
   }
+#if RT_SHADOW_ORDER
+          if (w_any) {   // a wave of any-hit rays: child order, no sort
+            uint32_t nxt = kDone;
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+              if (k[c] != INFINITY) {
+                if (nxt != kDone) push(nxt);
+                nxt = v[c];
+              }
+            cur = nxt == kDone ? pop() : nxt;
+          } else
+#endif
+          {
           RT_CSWAP(0, 1) RT_CSWAP(2, 3) RT_CSWAP(0, 2) RT_CSWAP(1, 3) RT_CSWAP(1, 2)
-#undef RT_CSWAP
           if (cnt == 0) {
             cur = pop();
           } else {
@@ -1300,6 +1318,8 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
             if (cnt > 1) push(v[1]);
             cur = v[0];
           }
+          }
+#undef RT_CSWAP
           if ((cur & kLeaf) && cur != kDone && pleaf == kDone) {   // first leaf: postpone, keep going
             pleaf = cur;
             cur = pop();
