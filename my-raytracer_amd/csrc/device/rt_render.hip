@@ -60,9 +60,6 @@ using namespace rtk;
 
 namespace {
 
-#ifndef RT_SHADOW_ORDER
-#define RT_SHADOW_ORDER 0   // A/B: 1 = waves of any-hit rays visit children in node order (no sort)
-#endif
 constexpr int kBlock = 256;        // threads per persistent block
 constexpr int kGroups = 8;          // work heads (XCD groups)
 constexpr int kRefill = 16;         // refill a wave when this many lanes are idle (8 / 32: +-0.2 %)
@@ -1168,9 +1165,10 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
       }
 
       uint32_t rounds = 0;
-#if RT_SHADOW_ORDER
+      // a wave whose traversing lanes are all any-hit rays visits children without the distance
+      // sort (any visit order finds the same occluded / not-occluded answer): office +3.6 %
+      // batched, +2.3 % one frame; config 4 +3.2 % one frame, -1.1 % batched (A/B)
       const bool w_any = wballot(!anyhit && cur != kDone) == 0;   // wave-uniform
-#endif
       while ((wballot(cur != kDone) | wballot(pleaf != kDone)) != 0) {
         if (++rounds > kTravGuard) {   // watchdog: abandon the round (results void, launch flagged)
           guard_trip();
@@ -1296,8 +1294,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
     const float tk = k[a]; k[a] = k[b]; k[b] = tk;            \
     const uint32_t tv = v[a]; v[a] = v[b]; v[b] = tv;         \
   }
-#if RT_SHADOW_ORDER
-          if (w_any) {   // a wave of any-hit rays: child order, no sort
+          if (w_any) {   // a wave of any-hit rays: the last hit child first, the others pushed
             uint32_t nxt = kDone;
 #pragma unroll
             for (int c = 0; c < 4; ++c)
@@ -1306,9 +1303,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
                 nxt = v[c];
               }
             cur = nxt == kDone ? pop() : nxt;
-          } else
-#endif
-          {
+          } else {
           RT_CSWAP(0, 1) RT_CSWAP(2, 3) RT_CSWAP(0, 2) RT_CSWAP(1, 3) RT_CSWAP(1, 2)
           if (cnt == 0) {
             cur = pop();
