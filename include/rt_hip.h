@@ -222,10 +222,7 @@ typedef struct rt_upload_options {
                             (32 = one XCD's worth: the smallest reservation a 256-VGPR kernel was
                             measured to run beside); 0 = none (default; rt_multi_create: 32 per GPU at
                             N > 1); -1 = none */
-  int child_order;       /* order of a wide node's children (A/B): 0 = the collapse's order (default), 1 = by
-                            increasing box area, 2 = by decreasing box area.  Any-hit waves visit a node's
-                            hit children last-first; closest-hit rays sort by distance either way */
-  int reserved_[6];
+  int reserved_[7];
 } rt_upload_options;
 
 /* Fills *opt with the defaults listed above. */

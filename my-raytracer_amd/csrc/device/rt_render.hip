@@ -1041,44 +1041,6 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
       auto ring = [&](uint32_t q) -> __attribute__((address_space(3))) uint32_t& {
         return *reinterpret_cast<__attribute__((address_space(3))) uint32_t*>((size_t)((q & kRingBMask) | lane_b));
       };
-#ifndef RT_AB_TOS
-#define RT_AB_TOS 0
-#endif
-#if RT_AB_TOS
-      auto ring_push = [&](uint32_t x) {
-        if (sq == sqlim) {   // ring full: its bottom entry goes to the spill stack
-          const uint32_t qlo = sqlim - kRingB;
-          spill[(size_t)(qlo / kSW) * P.nslots] = ring(qlo);
-          sqlim += kSW;
-          if (STATS) d_spills++;
-          if constexpr (TL) tl_spill++;
-        }
-        ring(sq) = x;
-        sq += kSW;
-      };
-      auto ring_pop = [&]() -> uint32_t {
-        if (sq == 0) return kDone;
-        sq -= kSW;
-        if (sq + kRingB >= sqlim) return ring(sq);
-        sqlim = sq + kRingB;
-        return spill[(size_t)(sq / kSW) * P.nslots];
-      };
-      // the top stack entry cached in a register: a pop right after a push (the far child after a
-      // near subtree that ended) does not wait on an LDS read
-      uint32_t tos = kDone;
-      auto push = [&](uint32_t x) {
-        if (tos != kDone) ring_push(tos);
-        tos = x;
-      };
-      auto pop = [&]() -> uint32_t {
-        if (tos != kDone) {
-          const uint32_t r = tos;
-          tos = kDone;
-          return r;
-        }
-        return ring_pop();
-      };
-#else
       auto push = [&](uint32_t x) {
         if (sq == sqlim) {   // ring full: its bottom entry goes to the spill stack
           const uint32_t qlo = sqlim - kRingB;
@@ -1097,7 +1059,6 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
         sqlim = sq + kRingB;
         return spill[(size_t)(sq / kSW) * P.nslots];
       };
-#endif
       const D3 c3 = d3(-rd.x, -rd.y, -rd.z);
 
       // Watchdog of the traversal loops that could cycle on a corrupt hierarchy (the round loop
@@ -1219,10 +1180,6 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
           // few lanes left and work to fetch: park the rest, shade and refill, resume next phase
           if (heads_left > 0 && __popcll(wballot(cur != kDone) | wballot(pleaf != kDone)) <= kSuspActive) {
             if (cur != kDone || pleaf != kDone) {
-#if RT_AB_TOS
-              if (tos != kDone) ring_push(tos);   // the parked stack lives in the ring / spill area only
-              tos = kDone;
-#endif
               const unsigned long long w0 = (unsigned long long)cur | ((unsigned long long)pleaf << 32);
               const unsigned long long w1 = (unsigned long long)((sq / kSW) | (((sqlim - kRingB) / kSW) << 16) |
                                                                   (shadow_hit ? 0x80000000u : 0u)) |
@@ -1283,11 +1240,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
           float4 nx, fx, ny, fy, nz, fz;
           uint4 rf;
           // wave-uniform: every active lane's node is in the LDS treelet -> ds_read, no TD cost
-#ifndef RT_AB_LATEREF
-#define RT_AB_LATEREF 0
-#endif
-          const bool in_lds = wballot(cur >= (uint32_t)P.n_top) == 0;
-          if (in_lds) {
+          if (wballot(cur >= (uint32_t)P.n_top) == 0) {
             if (STATS) wave_tick(d_node_lds, d_dummy, lane);
             if constexpr (TL) tl_wave_gap(2);
             const unsigned char* lb = lds_raw + P.top_off + cur * (uint32_t)sizeof(GNode4);
@@ -1317,11 +1270,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
             fy = *reinterpret_cast<const float4*>(RT_NODE_AT(nyo ^ 16u));
             nz = *reinterpret_cast<const float4*>(RT_NODE_AT(nzo));
             fz = *reinterpret_cast<const float4*>(RT_NODE_AT(nzo ^ 16u));
-#if RT_AB_LATEREF
-            rf = make_uint4(0u, 0u, 0u, 0u);
-#else
             rf = *reinterpret_cast<const uint4*>(RT_NODE_AT(96u));
-#endif
 #undef RT_NODE_AT
           }
 #pragma unroll
@@ -1334,32 +1283,18 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
             // the loop-carried bound made the compiler re-canonicalise it every iteration (2 VALU)
             const float tn = fmaxf(fmaxf(tx0, ty0), __builtin_amdgcn_fmed3f(tz0, lo_c, pinf));
             const float tf = fminf(fminf(tx1, ty1), __builtin_amdgcn_fmed3f(tz1, hi_c, -pinf));
-#if !RT_AB_LATEREF
             const uint32_t r = u4c(rf, c);
-#endif
             const bool h = tn <= tf;   // absent children carry the empty box [+inf, -inf]
             k[c] = h ? tn : INFINITY;
-#if !RT_AB_LATEREF
             v[c] = r;
-#endif
             cnt += h ? 1 : 0;
           }
-#if RT_AB_LATEREF
-          if (!in_lds && cnt > 0)   // child refs only for lanes that hit a child
-            rf = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(P.nodes4) +
-                                                 (uint32_t)(cur * (uint32_t)sizeof(GNode4) + 96u));
-#pragma unroll
-          for (int c = 0; c < 4; ++c) v[c] = u4c(rf, c);
-#endif
 #define RT_CSWAP(a, b)                                        \
   if (k[b] < k[a]) {                                          \
     const float tk = k[a]; k[a] = k[b]; k[b] = tk;            \
     const uint32_t tv = v[a]; v[a] = v[b]; v[b] = tv;         \
   }
-#ifndef RT_AB_SORTSKIP
-#define RT_AB_SORTSKIP 0
-#endif
-          if (w_any || (RT_AB_SORTSKIP && wballot(cnt > 1) == 0)) {   // a wave of any-hit rays: the last hit child first, the others pushed
+          if (w_any) {   // a wave of any-hit rays: the last hit child first, the others pushed
             uint32_t nxt = kDone;
 #pragma unroll
             for (int c = 0; c < 4; ++c)

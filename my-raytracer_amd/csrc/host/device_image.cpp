@@ -916,7 +916,6 @@ int build_image(const rt_scene_soa* s, const rt_bvh_soa* b, const rt_upload_opti
   if (opt.collapse != RT_COLLAPSE_GREEDY && opt.collapse != RT_COLLAPSE_SAH)
     return fail(RT_ERR_INVALID, "rt_scene_upload: unknown collapse");
   if (opt.build_threads < 0) return fail(RT_ERR_INVALID, "rt_scene_upload: build_threads < 0");
-  if (opt.child_order < 0 || opt.child_order > 2) return fail(RT_ERR_INVALID, "rt_scene_upload: child_order must be 0, 1 or 2");
   g_threads = opt.build_threads > 0 ? std::min(opt.build_threads, 64) : std::max(1, std::min(usable_cpus(), 64));
   g_verbose = opt.verbose != 0;
   const bool timing = g_verbose;   // phase times to stderr (diagnostics)
@@ -1112,12 +1111,7 @@ int build_image(const rt_scene_soa* s, const rt_bvh_soa* b, const rt_upload_opti
       auto assign = [&](int n) {
         g4[n] = (int)order.size();
         order.push_back(n);
-        Kids k = kids_of(n);
-        if (opt.child_order != 0)
-          std::stable_sort(k.c, k.c + k.n, [&](int a, int b) {
-            return opt.child_order == 1 ? area(a) < area(b) : area(a) > area(b);
-          });
-        kids.push_back(k);
+        kids.push_back(kids_of(n));
       };
       assign(0);
       for (size_t q = 0; q < order.size() && (int)order.size() < bfs_top; ++q) {   // breadth-first top
