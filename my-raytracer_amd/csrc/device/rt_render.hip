@@ -1234,8 +1234,17 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
             tl_it++; wave_tick(tl_wn, tl_dummy, lane);
           }
           if (STATS) { c_nodes++; wave_tick(d_node_it, d_node_ln, lane); wave_distinct(cur, d_node_lines, lane); }
+#ifndef RT_AB_HBITS
+#define RT_AB_HBITS 0
+#endif
+#ifndef RT_AB_PUSHFAST
+#define RT_AB_PUSHFAST 0
+#endif
           float k[4];
           uint32_t v[4];
+#if RT_AB_HBITS
+          bool hb[4];
+#endif
           int cnt = 0;
           float4 nx, fx, ny, fy, nz, fz;
           uint4 rf;
@@ -1285,6 +1294,9 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
             const float tf = fminf(fminf(tx1, ty1), __builtin_amdgcn_fmed3f(tz1, hi_c, -pinf));
             const uint32_t r = u4c(rf, c);
             const bool h = tn <= tf;   // absent children carry the empty box [+inf, -inf]
+#if RT_AB_HBITS
+            hb[c] = h;
+#endif
             k[c] = h ? tn : INFINITY;
             v[c] = r;
             cnt += h ? 1 : 0;
@@ -1298,7 +1310,11 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
             uint32_t nxt = kDone;
 #pragma unroll
             for (int c = 0; c < 4; ++c)
+#if RT_AB_HBITS
+              if (hb[c]) {
+#else
               if (k[c] != INFINITY) {
+#endif
                 if (nxt != kDone) push(nxt);
                 nxt = v[c];
               }
@@ -1308,9 +1324,18 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
           if (cnt == 0) {
             cur = pop();
           } else {
+#if RT_AB_PUSHFAST
+            if (wballot(sq + 3u * kSW > sqlim) == 0) {   // no lane can fill its ring with 3 pushes
+              if (cnt > 3) { ring(sq) = v[3]; sq += kSW; }
+              if (cnt > 2) { ring(sq) = v[2]; sq += kSW; }
+              if (cnt > 1) { ring(sq) = v[1]; sq += kSW; }
+            } else
+#endif
+            {
             if (cnt > 3) push(v[3]);
             if (cnt > 2) push(v[2]);
             if (cnt > 1) push(v[1]);
+            }
             cur = v[0];
           }
           }
