@@ -1038,6 +1038,9 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
           hi_c = round_up_f(tlim - t_off);
         }
       }
+#ifndef RT_AB_POPFAST
+#define RT_AB_POPFAST 0
+#endif
       auto ring = [&](uint32_t q) -> __attribute__((address_space(3))) uint32_t& {
         return *reinterpret_cast<__attribute__((address_space(3))) uint32_t*>((size_t)((q & kRingBMask) | lane_b));
       };
@@ -1053,6 +1056,14 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
         sq += kSW;
       };
       auto pop = [&]() -> uint32_t {
+#if RT_AB_POPFAST
+        if (wballot(sq != 0 && sq - kSW + kRingB < sqlim) == 0) {   // no active lane reads its spill area
+          const uint32_t r = ring(sq - kSW);   // (sq == 0: some ring word, discarded)
+          const bool e = sq == 0;
+          sq = e ? 0u : sq - kSW;
+          return e ? kDone : r;
+        }
+#endif
         if (sq == 0) return kDone;
         sq -= kSW;
         if (sq + kRingB >= sqlim) return ring(sq);
