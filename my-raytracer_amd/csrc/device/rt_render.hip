@@ -1038,9 +1038,6 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
           hi_c = round_up_f(tlim - t_off);
         }
       }
-#ifndef RT_AB_POPFAST
-#define RT_AB_POPFAST 0
-#endif
       auto ring = [&](uint32_t q) -> __attribute__((address_space(3))) uint32_t& {
         return *reinterpret_cast<__attribute__((address_space(3))) uint32_t*>((size_t)((q & kRingBMask) | lane_b));
       };
@@ -1056,14 +1053,6 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
         sq += kSW;
       };
       auto pop = [&]() -> uint32_t {
-#if RT_AB_POPFAST
-        if (wballot(sq != 0 && sq - kSW + kRingB < sqlim) == 0) {   // no active lane reads its spill area
-          const uint32_t r = ring(sq - kSW);   // (sq == 0: some ring word, discarded)
-          const bool e = sq == 0;
-          sq = e ? 0u : sq - kSW;
-          return e ? kDone : r;
-        }
-#endif
         if (sq == 0) return kDone;
         sq -= kSW;
         if (sq + kRingB >= sqlim) return ring(sq);
@@ -1178,7 +1167,9 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
       uint32_t rounds = 0;
       // a wave whose traversing lanes are all any-hit rays visits children without the distance
       // sort (any visit order finds the same occluded / not-occluded answer): office +3.6 %
-      // batched, +2.3 % one frame; config 4 +3.2 % one frame, -1.1 % batched (A/B)
+      // batched, +2.3 % one frame; config 4 +3.2 % one frame, -1.1 % batched; testing the hit bits
+      // instead of the keys (which then serve only the sorted path): office +2.1 % / +2.0 % more
+      // (A/B)
       const bool w_any = wballot(!anyhit && cur != kDone) == 0;   // wave-uniform
       while ((wballot(cur != kDone) | wballot(pleaf != kDone)) != 0) {
         if (++rounds > kTravGuard) {   // watchdog: abandon the round (results void, launch flagged)
@@ -1245,17 +1236,9 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
             tl_it++; wave_tick(tl_wn, tl_dummy, lane);
           }
           if (STATS) { c_nodes++; wave_tick(d_node_it, d_node_ln, lane); wave_distinct(cur, d_node_lines, lane); }
-#ifndef RT_AB_HBITS
-#define RT_AB_HBITS 0
-#endif
-#ifndef RT_AB_PUSHFAST
-#define RT_AB_PUSHFAST 0
-#endif
           float k[4];
           uint32_t v[4];
-#if RT_AB_HBITS
-          bool hb[4];
-#endif
+          bool hb[4];   // child hit (any-hit waves test these; the keys and count then serve only the sort)
           int cnt = 0;
           float4 nx, fx, ny, fy, nz, fz;
           uint4 rf;
@@ -1305,9 +1288,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
             const float tf = fminf(fminf(tx1, ty1), __builtin_amdgcn_fmed3f(tz1, hi_c, -pinf));
             const uint32_t r = u4c(rf, c);
             const bool h = tn <= tf;   // absent children carry the empty box [+inf, -inf]
-#if RT_AB_HBITS
             hb[c] = h;
-#endif
             k[c] = h ? tn : INFINITY;
             v[c] = r;
             cnt += h ? 1 : 0;
@@ -1321,11 +1302,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
             uint32_t nxt = kDone;
 #pragma unroll
             for (int c = 0; c < 4; ++c)
-#if RT_AB_HBITS
               if (hb[c]) {
-#else
-              if (k[c] != INFINITY) {
-#endif
                 if (nxt != kDone) push(nxt);
                 nxt = v[c];
               }
@@ -1335,18 +1312,9 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
           if (cnt == 0) {
             cur = pop();
           } else {
-#if RT_AB_PUSHFAST
-            if (wballot(sq + 3u * kSW > sqlim) == 0) {   // no lane can fill its ring with 3 pushes
-              if (cnt > 3) { ring(sq) = v[3]; sq += kSW; }
-              if (cnt > 2) { ring(sq) = v[2]; sq += kSW; }
-              if (cnt > 1) { ring(sq) = v[1]; sq += kSW; }
-            } else
-#endif
-            {
             if (cnt > 3) push(v[3]);
             if (cnt > 2) push(v[2]);
             if (cnt > 1) push(v[1]);
-            }
             cur = v[0];
           }
           }
