@@ -1,6 +1,6 @@
 """Interleaved A/B of kernel libraries on single-frame and batched frame time (dev tool, under
 gpurun).  usage: python tools/ab_frame.py ROUNDS lib1 lib2 ... [-- scene [tris]]
-A library entry may carry upload options after '#': lib.so#node_width=8,stack_ring=16."""
+A library entry may carry upload options after '#': lib.so#stack_ring=16,lds_treelet=-1."""
 import json
 import os
 import subprocess
