@@ -30,4 +30,5 @@ for r in range(R):
 for l, v in res.items():
     s = np.median([d["single_ms"] for d in v])
     b = np.median([d["batched_ms_per_frame"] for d in v])
-    print(f"{os.path.basename(l):48s} single {s:.4f} ms   batched {b:.4f} ms/frame", flush=True)
+    c = np.median([d.get("single_call_ms", float("nan")) for d in v])
+    print(f"{os.path.basename(l):48s} single {s:.4f} ms (call {c:.4f})   batched {b:.4f} ms/frame", flush=True)

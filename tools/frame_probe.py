@@ -1,6 +1,6 @@
 """One kernel library, office 1080p (dev tool, under gpurun; run by tools/ab_frame.py with
 RTAMD_HIP_LIB set): median kernel time of single-frame launches and of 64-frame launches
-(per frame), printed as one JSON line.  RTAMD_AB_OPTS: upload options "key=value,..."."""
+(per frame), printed as one JSON line; single_call_ms: HIP events around the one-frame call.  RTAMD_AB_OPTS: upload options "key=value,..."."""
 import json
 import os
 import sys
@@ -21,10 +21,15 @@ p = host.render_params(1920, 1080, 1)
 out = [torch.zeros((1080, 1920, 3), device="cuda") for _ in range(64)]
 for _ in range(5):
     gpu.launch(p, out[0].data_ptr())
-single = []
+single, call = [], []
 for _ in range(30):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
     gpu.launch(p, out[0].data_ptr())
+    e1.record()
     single.append(gpu.last_kernel_ms())
+    torch.cuda.synchronize()
+    call.append(e0.elapsed_time(e1))   # the whole call on the stream: set-up + kernel
 cams = [rtamd.camera_orbit(p, 0.12 * (f / 63 - 0.5)) for f in range(64)]
 gpu.launch_frames(cams, [o.data_ptr() for o in out])
 batch = []
@@ -32,4 +37,5 @@ for _ in range(3):
     gpu.launch_frames(cams, [o.data_ptr() for o in out])
     batch.append(gpu.last_kernel_ms() / 64)
 print(json.dumps({"single_ms": float(np.median(single)), "single_p90": float(np.percentile(single, 90)),
+                  "single_call_ms": float(np.median(call)),
                   "batched_ms_per_frame": float(np.median(batch))}), flush=True)
