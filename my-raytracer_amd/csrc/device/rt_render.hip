@@ -2036,27 +2036,6 @@ int fail(int code, const std::string& msg) {
   } while (0)
 
 
-// Launch control block set-up without a host-to-device copy: one small kernel on the launch stream,
-// its arguments carrying the frames, zeroes the counters and work heads and writes the frame table
-// (launches of up to kArgFrames frames; more frames keep the staged copy).  A small H2D copy on the
-// launch stream is a copy-engine command the render kernel then waits for; a kernel stays on the
-// compute queue ("launch set-up").
-#ifndef RT_CTL_KERNEL
-#define RT_CTL_KERNEL 1
-#endif
-constexpr int kArgFrames = 16;
-struct CtlArgs {
-  FrameDesc f[kArgFrames];
-  unsigned long long* ctr;
-  int n;
-};
-static_assert(sizeof(CtlArgs) <= 2048, "kernel arguments");
-__global__ void __launch_bounds__(256) ctl_setup_kernel(CtlArgs a) {
-  for (int i = threadIdx.x; i < (int)(kCtrBytes / sizeof(unsigned long long)); i += 256) a.ctr[i] = 0ull;
-  FrameDesc* fd = reinterpret_cast<FrameDesc*>(reinterpret_cast<unsigned char*>(a.ctr) + kCtrBytes);
-  if (threadIdx.x < a.n) fd[threadIdx.x] = a.f[threadIdx.x];
-}
-
 using KernelFn = void (*)(KParams);
 
 struct Variant {
@@ -2702,30 +2681,18 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
     HIP_TRY(hipStreamWaitEvent(st, C.ev1, 0));   // previous launch on this context done (device side)
     HIP_TRY(hipEventSynchronize(C.ev1));         // ... and its staged copy consumed (host side)
   }
-  // zeroed counters + frame table: the set-up kernel (up to kArgFrames frames), else one copy from
-  // the context's pinned staging
-  auto frame_desc = [&](FrameDesc& d, int f) {
-    std::memset(&d, 0, sizeof(FrameDesc));
+  // zeroed counters + frame table, one copy from the context's pinned staging
+  std::memset(C.h_ctl, 0, kCtrBytes);
+  FrameDesc* fd = reinterpret_cast<FrameDesc*>(C.h_ctl + kCtrBytes);
+  for (int f = 0; f < n_frames; ++f) {
+    std::memset(&fd[f], 0, sizeof(FrameDesc));
     for (int k = 0; k < 3; ++k) {
-      d.eye[k] = p[f].camera.eye[k]; d.ll[k] = p[f].camera.lower_left[k];
-      d.xd[k] = p[f].camera.x_dir[k]; d.yd[k] = p[f].camera.y_dir[k];
+      fd[f].eye[k] = p[f].camera.eye[k]; fd[f].ll[k] = p[f].camera.lower_left[k];
+      fd[f].xd[k] = p[f].camera.x_dir[k]; fd[f].yd[k] = p[f].camera.y_dir[k];
     }
-    d.out = outs[f];
-  };
-  if (RT_CTL_KERNEL && n_frames <= kArgFrames) {
-    CtlArgs a;
-    std::memset(&a, 0, sizeof a);
-    for (int f = 0; f < n_frames; ++f) frame_desc(a.f[f], f);
-    a.ctr = C.d_ctr;
-    a.n = n_frames;
-    hipLaunchKernelGGL(ctl_setup_kernel, dim3(1), dim3(256), 0, st, a);
-    HIP_TRY(hipGetLastError());
-  } else {
-    std::memset(C.h_ctl, 0, kCtrBytes);
-    FrameDesc* fd = reinterpret_cast<FrameDesc*>(C.h_ctl + kCtrBytes);
-    for (int f = 0; f < n_frames; ++f) frame_desc(fd[f], f);
-    HIP_TRY(hipMemcpyAsync(C.d_ctr, C.h_ctl, kCtrBytes + (size_t)n_frames * sizeof(FrameDesc), hipMemcpyHostToDevice, st));
+    fd[f].out = outs[f];
   }
+  HIP_TRY(hipMemcpyAsync(C.d_ctr, C.h_ctl, kCtrBytes + (size_t)n_frames * sizeof(FrameDesc), hipMemcpyHostToDevice, st));
   if (v == 3) {   // round timeline: zeroed, so unused records read as t = 0
     const size_t tb = sc->nslots / 64 * kTlCap * kTlWords * sizeof(unsigned long long);
     if (!C.d_tl) {
