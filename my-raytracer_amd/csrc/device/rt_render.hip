@@ -561,7 +561,11 @@ __device__ __forceinline__ uint32_t order_class(uint32_t cost) {
   const int q = (int)(__float_as_uint((float)cost) >> kOrderShift) - ((127 + 8) << (23 - kOrderShift));
   return 255u - (uint32_t)min(255, max(0, q));
 }
-__device__ void order_range(const uint32_t* cost, uint32_t* order, long long n_tiles, int h, unsigned char* lds) {
+#ifndef RT_ORDER_DILATE
+#define RT_ORDER_DILATE 0   // A/B: a tile's sort cost = the max over +-R tiles of its row (camera motion)
+#endif
+__device__ void order_range(const uint32_t* cost, uint32_t* order, long long n_tiles, int h, unsigned char* lds,
+                            int tiles_x) {
   using Sort = rocprim::block_radix_sort<unsigned int, kBlock, kOrderItems>;
   static_assert(sizeof(typename Sort::storage_type) <= 30720, "sort storage must fit the block's LDS (at least 30 KB)");
   auto& storage = *reinterpret_cast<typename Sort::storage_type*>(lds);
@@ -570,7 +574,21 @@ __device__ void order_range(const uint32_t* cost, uint32_t* order, long long n_t
 #pragma unroll
   for (int j = 0; j < kOrderItems; ++j) {
     const long long li = (long long)threadIdx.x * kOrderItems + j;   // local index in the range
+#if RT_ORDER_DILATE
+    uint32_t c = 0u;
+    if (t0 + li < t1) {
+      const long long t = t0 + li, row = t / tiles_x;
+      c = cost[t];
+      for (int k = 1; k <= RT_ORDER_DILATE; ++k) {
+        if (t - k >= 0 && (t - k) / tiles_x == row) c = max(c, cost[t - k]);
+        if (t + k < n_tiles && (t + k) / tiles_x == row) c = max(c, cost[t + k]);
+      }
+    }
+    keys[j] = t0 + li < t1 ? (order_class(c) << 12) | (uint32_t)li : 0xffffffffu;
+#else
+    (void)tiles_x;
     keys[j] = t0 + li < t1 ? (order_class(cost[t0 + li]) << 12) | (uint32_t)li : 0xffffffffu;   // padding last
+#endif
   }
   Sort().sort(keys, storage, 12, 20);
 #pragma unroll
@@ -1864,7 +1882,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
       __syncthreads();   // every thread has read it before the sort reuses the LDS
       if (j >= 2u * kGroups) break;
       if (j < (uint32_t)kGroups) {
-        if (P.order_src) order_range(P.order_src, P.next_order, P.n_pos, (int)j, lds_raw);
+        if (P.order_src) order_range(P.order_src, P.next_order, P.n_pos, (int)j, lds_raw, P.tiles_x);
       } else {
         for (long long i = P.n_pos * (j - kGroups) / kGroups + threadIdx.x; i < P.n_pos * (j - kGroups + 1) / kGroups;
              i += kBlock)

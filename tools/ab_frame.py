@@ -31,4 +31,6 @@ for l, v in res.items():
     s = np.median([d["single_ms"] for d in v])
     b = np.median([d["batched_ms_per_frame"] for d in v])
     c = np.median([d.get("single_call_ms", float("nan")) for d in v])
-    print(f"{os.path.basename(l):48s} single {s:.4f} ms (call {c:.4f})   batched {b:.4f} ms/frame", flush=True)
+    o = np.median([d.get("single_orbit20_ms", float("nan")) for d in v])
+    print(f"{os.path.basename(l):48s} single {s:.4f} ms (call {c:.4f}, orbit-20 views {o:.4f})   "
+          f"batched {b:.4f} ms/frame", flush=True)
