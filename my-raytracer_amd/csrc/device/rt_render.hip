@@ -575,14 +575,18 @@ __device__ void order_range(const uint32_t* cost, uint32_t* order, long long n_t
   for (int j = 0; j < kOrderItems; ++j) {
     const long long li = (long long)threadIdx.x * kOrderItems + j;   // local index in the range
 #if RT_ORDER_DILATE
+#ifndef RT_ORDER_DILATE_Y
+#define RT_ORDER_DILATE_Y 0
+#endif
     uint32_t c = 0u;
     if (t0 + li < t1) {
-      const long long t = t0 + li, row = t / tiles_x;
-      c = cost[t];
-      for (int k = 1; k <= RT_ORDER_DILATE; ++k) {
-        if (t - k >= 0 && (t - k) / tiles_x == row) c = max(c, cost[t - k]);
-        if (t + k < n_tiles && (t + k) / tiles_x == row) c = max(c, cost[t + k]);
-      }
+      const long long t = t0 + li, row = t / tiles_x, col = t - row * tiles_x;
+      const long long rows_n = (n_tiles + tiles_x - 1) / tiles_x;
+      for (long long r = max(0LL, row - RT_ORDER_DILATE_Y); r <= min(rows_n - 1, row + (long long)RT_ORDER_DILATE_Y); ++r)
+        for (long long x = max(0LL, col - RT_ORDER_DILATE); x <= min((long long)tiles_x - 1, col + (long long)RT_ORDER_DILATE); ++x) {
+          const long long u = r * tiles_x + x;
+          if (u < n_tiles) c = max(c, cost[u]);
+        }
     }
     keys[j] = t0 + li < t1 ? (order_class(c) << 12) | (uint32_t)li : 0xffffffffu;
 #else
