@@ -249,7 +249,7 @@ struct KParams {
   int row_begin, stripe_h, stripe_count, stripe_index;
   int rows;
   int tiles_x;
-  int pad1;
+  int order_dilate;         // cost-ordered launches: cost window half-width along a tile row (order_range)
   long long n_tiles;
   // list mode (adaptive pass): list entries are frame << 25 | local pixel id; work item w = one
   // sample (w % nsamp) of pixel list[w / nsamp] (a pixel's samples run on neighbouring lanes:
@@ -552,6 +552,7 @@ constexpr int kWavesPerEU = 4;   // 4 waves/SIMD = 16 waves/CU (register budget 
 // "cost-ordered tiles").  The order is built inside the render kernel by its first blocks to run
 // out of work, from the cost map of the launch before, so it costs no launch and no busy CU.
 constexpr int kOrderItems = 16;
+constexpr int kOrderDilate = 4;   // tiles (A/B: 2 / 4 / 8 along the row; 2-D windows slower, r04v)
 constexpr long long kOrderMaxRange = (long long)kBlock * kOrderItems;   // tiles per head range (4096)
 // Sort keys: a log-scale cost class (4 per octave from 2^8 ticks; 16 per octave: -1.5 %, 1 per
 // octave: +-0, profiles/r03/r03u_ab_order_*.txt) inverted so that higher costs sort first, above the
@@ -561,11 +562,14 @@ __device__ __forceinline__ uint32_t order_class(uint32_t cost) {
   const int q = (int)(__float_as_uint((float)cost) >> kOrderShift) - ((127 + 8) << (23 - kOrderShift));
   return 255u - (uint32_t)min(255, max(0, q));
 }
-#ifndef RT_ORDER_DILATE
-#define RT_ORDER_DILATE 0   // A/B: a tile's sort cost = the max over +-R tiles of its row (camera motion)
-#endif
+// dilate > 0: a tile's sort cost is the largest cost within +-dilate tiles of its tile row.  The
+// order then follows the expensive regions rather than single expensive tiles, which keeps the
+// costliest paths first when the camera moved since the costs were recorded (the frame two
+// launches back) and keeps neighbouring tiles together (stable sort): office 1080p one frame
+// -9 % (same view) / -13 % (driver-shape animation); random-triangle soups lose by it (-4 %),
+// so deep hierarchies keep the exact costs (DESIGN.md §4 "cost-ordered tiles")
 __device__ void order_range(const uint32_t* cost, uint32_t* order, long long n_tiles, int h, unsigned char* lds,
-                            int tiles_x) {
+                            int tiles_x, int dilate) {
   using Sort = rocprim::block_radix_sort<unsigned int, kBlock, kOrderItems>;
   static_assert(sizeof(typename Sort::storage_type) <= 30720, "sort storage must fit the block's LDS (at least 30 KB)");
   auto& storage = *reinterpret_cast<typename Sort::storage_type*>(lds);
@@ -574,25 +578,13 @@ __device__ void order_range(const uint32_t* cost, uint32_t* order, long long n_t
 #pragma unroll
   for (int j = 0; j < kOrderItems; ++j) {
     const long long li = (long long)threadIdx.x * kOrderItems + j;   // local index in the range
-#if RT_ORDER_DILATE
-#ifndef RT_ORDER_DILATE_Y
-#define RT_ORDER_DILATE_Y 0
-#endif
     uint32_t c = 0u;
     if (t0 + li < t1) {
       const long long t = t0 + li, row = t / tiles_x, col = t - row * tiles_x;
-      const long long rows_n = (n_tiles + tiles_x - 1) / tiles_x;
-      for (long long r = max(0LL, row - RT_ORDER_DILATE_Y); r <= min(rows_n - 1, row + (long long)RT_ORDER_DILATE_Y); ++r)
-        for (long long x = max(0LL, col - RT_ORDER_DILATE); x <= min((long long)tiles_x - 1, col + (long long)RT_ORDER_DILATE); ++x) {
-          const long long u = r * tiles_x + x;
-          if (u < n_tiles) c = max(c, cost[u]);
-        }
+      const long long x0 = max(0LL, col - dilate), x1 = min((long long)tiles_x - 1, col + dilate);
+      for (long long x = x0; x <= x1; ++x) c = max(c, cost[row * tiles_x + x]);
     }
-    keys[j] = t0 + li < t1 ? (order_class(c) << 12) | (uint32_t)li : 0xffffffffu;
-#else
-    (void)tiles_x;
-    keys[j] = t0 + li < t1 ? (order_class(cost[t0 + li]) << 12) | (uint32_t)li : 0xffffffffu;   // padding last
-#endif
+    keys[j] = t0 + li < t1 ? (order_class(c) << 12) | (uint32_t)li : 0xffffffffu;   // padding last
   }
   Sort().sort(keys, storage, 12, 20);
 #pragma unroll
@@ -1886,7 +1878,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
       __syncthreads();   // every thread has read it before the sort reuses the LDS
       if (j >= 2u * kGroups) break;
       if (j < (uint32_t)kGroups) {
-        if (P.order_src) order_range(P.order_src, P.next_order, P.n_pos, (int)j, lds_raw, P.tiles_x);
+        if (P.order_src) order_range(P.order_src, P.next_order, P.n_pos, (int)j, lds_raw, P.tiles_x, P.order_dilate);
       } else {
         for (long long i = P.n_pos * (j - kGroups) / kGroups + threadIdx.x; i < P.n_pos * (j - kGroups + 1) / kGroups;
              i += kBlock)
@@ -2665,6 +2657,7 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
       }
       if ((n_pos + kGroups - 1) / kGroups <= kOrderMaxRange) {   // the drain jobs: next order, next map cleared
         P.order_src = q >= 1 ? sc->d_cost[(q + 2) % 3] : nullptr;
+        P.order_dilate = sc->deep ? 0 : kOrderDilate;
         P.next_order = sc->d_order[(q + 1) % 2];
         P.zero_map = sc->d_cost[(q + 1) % 3];
         P.n_pos = n_pos;
