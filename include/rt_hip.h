@@ -222,7 +222,10 @@ typedef struct rt_upload_options {
                             (32 = one XCD's worth: the smallest reservation a 256-VGPR kernel was
                             measured to run beside); 0 = none (default; rt_multi_create: 32 per GPU at
                             N > 1); -1 = none */
-  int reserved_[7];
+  int order_window;      /* one-frame cost order (RT_FLAG_COST_ORDER, the default on one stream): a tile sorts by
+                            the largest recorded cost within +-order_window tiles of its row; 0 = by size (4,
+                            exact costs for hierarchies from 2^18 device records on; default), -1 = exact */
+  int reserved_[6];
 } rt_upload_options;
 
 /* Fills *opt with the defaults listed above. */

@@ -2175,6 +2175,7 @@ struct rt_scene {
   // rt_upload_options.reserve_cus: launches run on internal streams whose CU mask leaves that many
   // CUs free, one per caller stream (at most kMaskedStreams, then shared round robin)
   int reserve_cus = 0;
+  int order_window = 0;   // rt_upload_options.order_window (0: by depth)
   static constexpr int kMaskedStreams = 4;
   hipStream_t masked[kMaskedStreams] = {};
   hipStream_t masked_for[kMaskedStreams] = {};
@@ -2267,6 +2268,7 @@ int upload_image(const SceneImage& I, const rt_upload_options& opt, int device, 
   sc->bpc_cap = opt.blocks_per_cu;
   sc->grid_spare = opt.grid_spare;
   sc->reserve_cus = opt.reserve_cus;   // bounded by the CU count below
+  sc->order_window = opt.order_window;
   sc->delta = I.delta;
   for (int k = 0; k < 3; ++k) {
     sc->root_lo[k] = I.root_lo[k];
@@ -2338,6 +2340,8 @@ int resolve_options(const rt_upload_options* opt, rt_upload_options& o) {
   if (o.collapse_c_tri == 0.0) o.collapse_c_tri = d.collapse_c_tri;
   if (o.lds_treelet < -1) return fail(RT_ERR_INVALID, "rt_scene_upload: lds_treelet must be >= -1");
   if (o.reserve_cus < -1) return fail(RT_ERR_INVALID, "rt_scene_upload: reserve_cus must be >= -1");
+  if (o.order_window < -1 || o.order_window > 64)
+    return fail(RT_ERR_INVALID, "rt_scene_upload: order_window must be in [-1, 64]");
   if (o.stack_ring != 0 && o.stack_ring != 8 && o.stack_ring != 16)
     return fail(RT_ERR_INVALID, "rt_scene_upload: stack_ring must be 0, 8 or 16");
   if (o.blocks_per_cu < 0 || o.grid_spare < 0 || o.build_threads < 0)
@@ -2657,7 +2661,8 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
       }
       if ((n_pos + kGroups - 1) / kGroups <= kOrderMaxRange) {   // the drain jobs: next order, next map cleared
         P.order_src = q >= 1 ? sc->d_cost[(q + 2) % 3] : nullptr;
-        P.order_dilate = sc->deep ? 0 : kOrderDilate;
+        P.order_dilate = sc->order_window > 0 ? sc->order_window : sc->order_window < 0 ? 0
+                         : sc->deep ? 0 : kOrderDilate;
         P.next_order = sc->d_order[(q + 1) % 2];
         P.zero_map = sc->d_cost[(q + 1) % 3];
         P.n_pos = n_pos;

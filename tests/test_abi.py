@@ -82,12 +82,13 @@ def test_upload_options_defaults_and_validation():
     assert (o.device_tree, o.stack_ring, o.lds_treelet, o.collapse) == (abi.RT_TREE_SBVH, 0, 0, abi.RT_COLLAPSE_BY_SIZE)
     assert (o.sbvh_leaf_max, o.sbvh_bins, o.blocks_per_cu, o.grid_spare, o.verbose) == (0, 32, 0, 0, 0)
     assert (o.sbvh_alpha, o.sbvh_budget, o.sbvh_c_trav, o.collapse_c_tri) == (-1.0, -1.0, 1.0, 1.0)
+    assert (o.reserve_cus, o.order_window) == (0, 0)
     hs = rtamd.HostScene.generate("cornell")
     hs.prepare()
     lib = rtamd.hip_lib()
     for field, bad in (("stack_ring", 12), ("blocks_per_cu", -1), ("sbvh_bins", 1), ("sbvh_leaf_max", 9), ("sbvh_leaf_max", -1),
                        ("device_tree", 7), ("collapse", 3), ("sbvh_alpha", float("nan")), ("sbvh_budget", float("nan")),
-                       ("lds_treelet", -2), ("sbvh_c_trav", -1.0)):
+                       ("lds_treelet", -2), ("sbvh_c_trav", -1.0), ("order_window", -2), ("order_window", 65)):
         q = rtamd.upload_options(**{field: bad})
         rc = lib.rt_scene_upload_ex(hs.soa, hs.bvh, 0, C.byref(q), C.byref(C.c_void_p()))
         assert rc == abi.RT_ERR_INVALID, (field, rc)

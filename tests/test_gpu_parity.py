@@ -800,6 +800,24 @@ def test_device_tree_changes_no_pixel(kind, kw, w, h, spp):
           f"sbvh {wc.node_visits} / {wc.tri_tests}  reference {wb.node_visits} / {wb.tri_tests}")
 
 
+@pytest.mark.parametrize("window", [-1, 1, 8])
+def test_order_window_changes_no_pixel(window):
+    # rt_upload_options.order_window only changes which tiles a one-frame launch renders first
+    # (cost windows along the tile row): the images of consecutive cost-ordered launches equal the
+    # natural order's bit for bit, with the same ray counts.
+    hs, ref_dev, _ = Case.get("office")
+    dev = rtamd.DeviceScene(hs, 0, order_window=window)
+    base = hs.render_params(200, 113, 1)
+    for f in range(5):
+        p = rtamd.camera_orbit(base, 0.03 * f)
+        q = rtamd.abi.RenderParams.from_buffer_copy(p)
+        q.flags = rtamd.abi.RT_FLAG_NATURAL_ORDER
+        a, sa = dev.render(p)   # default one-frame launches on one stream: cost-ordered from the third
+        b, sb = ref_dev.render(q)
+        assert np.array_equal(a, b) and counts(sa) == counts(sb), f
+    dev.close()
+
+
 @pytest.mark.parametrize("tree", ["sah", "sbvh"])
 def test_tree_independent_of_build_threads(tree):
     hs = rtamd.HostScene.generate("random_tris", n_triangles=300000, seed=5)
