@@ -38,13 +38,21 @@ recursive unordered fp64 BVH traversal, closest-hit shadow rays, OpenMP on every
 CPU this process may use) timed on whole frames of the same workload, rank 0 /
 N=1 only.
 
+N > 1 (one process per GPU): under a launcher (torch.distributed.run sets WORLD_SIZE, which must
+equal --gpus), or without one: `python bench.py --gpus N` then starts the N ranks itself as child
+processes (torch.distributed.run, 127.0.0.1) before it makes any GPU call, and exits with their
+status; rank 0 prints the JSON line.  The N > 1 line carries a multi_gpu record: the render and
+gather time of each launch (HIP events on the launch stream, max over ranks) and the same run with
+the other reserve_cus setting (0 / 32 CUs left free for the gather).
+
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-       (N>1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
 """
 import argparse
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -62,6 +70,14 @@ HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # The CU's vector-L1 data return (TD): one 64-lane dwordx4 wave-instruction per 16 cycles =
 # 64 B/clk/CU (tools/l1_micro.hip) x 256 CUs x 2.4 GHz.
 L1_PEAK_GBPS = 64 * 256 * 2.4
+L1_PEAK_SOURCE = ("measured, not a datasheet figure (MI355X_MICROARCH.md gives none): tools/l1_micro.hip, an "
+                  "L1-resident dependent gather, 16 cycles of a CU's TD per 64-lane dwordx4 wave-instruction "
+                  "touching <= 16 lines = 64 B/clk/CU (profiles/r05/l1_micro_r05.txt)")
+# roofline.bound vocabulary: the resource whose measured fraction of its peak is at least
+# BOUND_FRAC ("hbm": HBM bytes, "l1": vector-L1 data return, "valu": VALU issue); none of them ->
+# "latency" (each wave's dependent chain of fetches and ALU at 4 waves per SIMD)
+BOUND_FRAC = 0.8
+BOUND_VOCAB = ("hbm", "l1", "valu", "latency")
 # VALU issue (MI355X_MICROARCH.md, "Per-instruction cycle constants"): a SIMD-32 issues a 32-bit
 # wave64 VALU instruction in 2 cycles (4 cycles is what ONE wave alone sustains), an fp64 one in 4
 # (16 lanes per cycle: 78.6 TF fp64 = half the fp32 rate), a transcendental in 8 (the issue-cost
@@ -115,10 +131,16 @@ def parse():
                          "reference median-split tree of BASELINE config 2, mybvh.cpp:375-539, and the SAH tree) "
                          "and report each with its upload / build seconds (tree_records); auto = on for one GPU, "
                          "scenes below 2^20 triangles, no --adaptive")
-    ap.add_argument("--reserve-cus", type=int, default=-2,
+    ap.add_argument("--reserve-cus", type=int, default=0,
                     help="rt_upload_options.reserve_cus: CUs each render launch leaves free (its grid on an internal "
-                         "CU-masked stream), so the RCCL gather of the previous launch runs beside it instead of "
-                         "after it (DESIGN.md §8); default 32 (one XCD's worth) on N > 1, 0 on one GPU")
+                         "CU-masked stream), so the RCCL gather of the previous launch can run beside it instead of "
+                         "after it (DESIGN.md §8); default 0 (32 = one XCD's worth costs ~12 %% of the render)")
+    ap.add_argument("--reserve-ab", choices=["auto", "on", "off"], default="auto",
+                    help="N > 1: after the timed run, time the same run again with the other reserve_cus setting "
+                         "(32 if the run used 0, else 0) and report both (multi_gpu.reserve_cus_ab); auto = on at N > 1")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="start the ranks (--gpus N), join a gloo process group, check its size, print one JSON line "
+                         "and exit before any GPU call (a dry run of the N-rank launch)")
     ap.add_argument("--opt", action="append", default=[], metavar="FIELD=VALUE",
                     help="dev A/B: an rt_upload_options field (e.g. lds_treelet=9); pixels are identical")
     ap.add_argument("--analytic", action="store_true",
@@ -136,14 +158,70 @@ def workload_key(a, n):
             "analytic": bool(a.analytic or a.scene == "spheres"), "n_gpus": n}
 
 
+def free_port():
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def spawn_ranks(a):
+    """--gpus N > 1 without a launcher: start the N ranks as children of this process
+    (python -m torch.distributed.run, rendezvous on 127.0.0.1) and return their exit status.
+    Called before this process makes any GPU call (torch.cuda.device_count() does not initialise
+    the GPU on this image), and the ranks are child processes, not an exec of this one.  Rank 0's
+    JSON line reaches this process's stdout.  Fewer visible GPUs than N is an error (exit 2),
+    unless RT_BENCH_DEVICE pins every rank to one device (dev rehearsal with --dist-backend gloo)."""
+    if "RT_BENCH_DEVICE" not in os.environ and not a.launch_check:
+        have = torch.cuda.device_count()
+        if have < a.gpus:
+            print(f"bench.py: --gpus {a.gpus} but {have} GPU(s) visible", file=sys.stderr, flush=True)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), str(Path(__file__).resolve()),
+           *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC (RCCL across processes)
+    env.setdefault("OMP_NUM_THREADS", str(max(1, usable_cpus() // a.gpus)))
+    return subprocess.run(cmd, env=env).returncode
+
+
+def launch_check(a, n, rank):
+    """--launch-check: the ranks exist and agree on the world size; no GPU call."""
+    ws = 1
+    if n > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo")
+        ws = dist.get_world_size()
+        ranks = [None] * ws
+        dist.all_gather_object(ranks, (rank, os.getpid()))
+    else:
+        ranks = [(0, os.getpid())]
+    if ws != a.gpus:
+        raise SystemExit(f"bench.py: world size {ws} but --gpus {a.gpus}")
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": ws, "ranks": sorted(r for r, _ in ranks),
+                          "distinct_pids": len({p for _, p in ranks}), "parent_pid": os.getppid()}), flush=True)
+    if n > 1:
+        dist.destroy_process_group()
+
+
 def main():
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" in os.environ:   # under a launcher: one process per GPU
+        world = int(os.environ["WORLD_SIZE"])
+        if world != a.gpus:
+            raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE {world}")
+    elif a.gpus > 1:                 # no launcher: start the ranks, before any GPU call
+        sys.exit(spawn_ranks(a))
+    else:
+        world = 1
+    if a.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if a.gpus != world and world > 1:
-        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE {world}")
     n = world
+    if a.launch_check:
+        return launch_check(a, n, rank)
     # rehearsal of the N-rank path on fewer GPUs (dev only): --dist-backend gloo stages the
     # collectives through host memory and RT_BENCH_DEVICE pins every rank to one device
     dev = int(os.environ.get("RT_BENCH_DEVICE", local))
@@ -154,6 +232,8 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group("gloo")
+        if dist.get_world_size() != a.gpus:
+            raise SystemExit(f"bench.py: process group of {dist.get_world_size()} ranks but --gpus {a.gpus}")
     host_staged = a.dist_backend == "gloo"
 
     # ---- host side: scene, normals, SoA, median-split BVH (untimed) ----
@@ -270,6 +350,7 @@ def main():
     image = None
 
     starts, ends, launch_frames = [], [], []
+    gstarts, gends = [], []   # N > 1: HIP events around each launch's gather + re-interleave
 
     def launch(li, nf, timed, flags=0):
         """Launch li renders nf frames (steps); their stripes are then gathered to rank 0.  A one-frame
@@ -300,7 +381,14 @@ def main():
                 ends.append(e1)
                 launch_frames.append(nf)
             # N>1: ONE RCCL gather of the nf frames' stripes + re-interleave
+            if timed and n > 1:
+                g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                g0.record(s)
             image = gathers[li % S](fbufs[li % S][:nf])
+            if timed and n > 1:
+                g1.record(s)   # the gather's end: the stream waits for the collective (and rank 0's copies)
+                gstarts.append(g0)
+                gends.append(g1)
 
     def run(steps, timed, per_launch=F, flags=0):
         li, done = 0, 0
@@ -325,12 +413,41 @@ def main():
             dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         return float(tmax[0])
 
-    run(a.warmup, False)
-    elapsed = timed_region(lambda: run(a.steps, True))
-    kernel_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
-    kernel_ms_avg = float(np.mean(kernel_ms))
+    def timed_run(warm):
+        """warm-up frames, then the timed run of a.steps frames: (seconds (max over ranks), mean
+        launch ms, mean gather ms); the per-launch event lists are refilled."""
+        for lst in (starts, ends, launch_frames, gstarts, gends):
+            lst.clear()
+        run(warm, False)
+        el = timed_region(lambda: run(a.steps, True))
+        k_ms = float(np.mean([s_.elapsed_time(e_) for s_, e_ in zip(starts, ends)]))
+        g_ms = float(np.mean([s_.elapsed_time(e_) for s_, e_ in zip(gstarts, gends)])) if gstarts else 0.0
+        return el, k_ms, g_ms
+
+    elapsed, kernel_ms_avg, gather_ms_avg = timed_run(a.warmup)
     frames_per_launch = float(np.mean(launch_frames))
     last_image = image
+
+    def over_ranks(vals):
+        """[max over ranks, rank 0's] of each value (N > 1)."""
+        t = torch.tensor(vals, dtype=torch.float64, device="cuda")
+        r0 = t.clone()
+        if n > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dist.broadcast(r0, src=0)
+        return [(float(x), float(y)) for x, y in zip(t, r0)]
+
+    multi = None
+    if n > 1:
+        (k_max, k_r0), (g_max, g_r0) = over_ranks([kernel_ms_avg, gather_ms_avg])
+        multi = {"render_ms_per_launch_max": round(k_max, 4), "render_ms_per_launch_rank0": round(k_r0, 4),
+                 "gather_ms_per_launch_rank0": round(g_r0, 4), "gather_ms_per_launch_max": round(g_max, 4),
+                 "frames_per_launch": frames_per_launch,
+                 "gather_MB_per_launch_into_rank0": round((n - 1) * frames_per_launch * rows_max * W * 3 * 4 / 1e6, 2),
+                 "reserve_cus": int(upload_opts.get("reserve_cus", 0)),
+                 "def": "render = HIP events around each launch on its stream; gather = HIP events around the "
+                        "collective of its frames' stripes + rank 0's re-interleave (includes waiting for the "
+                        "slowest rank's render); means over the timed launches, then max over ranks"}
 
     # single-frame record: the reference's use, one frame per launch (mytracer_gpu.cu:59-81)
     # (NS consecutive views of the orbit, one per launch) in the natural tile order, then with the
@@ -339,7 +456,8 @@ def main():
     single = None
     if a.single_frames > 0 and not a.adaptive:
         def single_record(flags):
-            starts.clear(); ends.clear(); launch_frames.clear()
+            for lst in (starts, ends, launch_frames, gstarts, gends):
+                lst.clear()
             el = timed_region(lambda: run(NS, True, per_launch=1, flags=flags))
             return {"frames": NS, "rays_per_frame": None, "ms_per_frame": round(el / NS * 1e3, 4),
                     "kernel_ms_avg": round(float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)])), 4)}
@@ -366,6 +484,24 @@ def main():
     if n > 1:
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
     rays_total, rays_frame0 = float(tot[0]), float(tot[1])
+
+    # N > 1: the same run with the other reserve_cus setting (0 <-> 32 CUs left free for the
+    # gather), so every N > 1 line measures what the reservation costs the render and what it
+    # gains the gather overlap -- same scene, same launches, pixels identical
+    if multi is not None and (a.reserve_ab == "on" or (a.reserve_ab == "auto" and not a.adaptive)):
+        main_r = multi["reserve_cus"]
+        other = 32 if main_r <= 0 else 0
+        gpu.close()
+        gpu = rtamd.DeviceScene(host, device=dev, analytic=a.analytic or a.scene == "spheres", tree=a.tree,
+                                **dict(upload_opts, reserve_cus=other))
+        el2, k2, g2 = timed_run(min(a.warmup, F))
+        (el2_max, _), (k2_max, _), (g2_max, g2_r0) = over_ranks([el2, k2, g2])
+        rec = {str(main_r): {"value": round(rays_total / elapsed / 1e6, 2), "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+                             "render_ms_per_launch_max": multi["render_ms_per_launch_max"],
+                             "gather_ms_per_launch_rank0": multi["gather_ms_per_launch_rank0"]},
+               str(other): {"value": round(rays_total / el2_max / 1e6, 2), "ms_per_step": round(el2_max / a.steps * 1e3, 4),
+                            "render_ms_per_launch_max": round(k2_max, 4), "gather_ms_per_launch_rank0": round(g2_r0, 4)}}
+        multi["reserve_cus_ab"] = rec
 
     if rank == 0:
         if a.save:
@@ -394,23 +530,28 @@ def main():
             "frames_per_launch": frames_per_launch,
             "note": "achieved = HBM bytes per launch (rocprofv3 FETCH_SIZE/WRITE_SIZE of this workload, per frame, "
                     "x frames per launch; traffic) / mean launch duration (HIP events on the launch stream); "
-                    "frac = achieved / 8 TB/s.  The kernel is not HBM-bound: the scene is cache-resident; each wave "
-                    "is bound by its own dependent chain (node fetch, box test, stack pop) at 4 waves per SIMD "
-                    "(wave_cycles; l1_roof prices the vector-L1 data path; DESIGN.md §4-5)",
-            # SURVEY §8d canonical work: 64 B per 2-wide node + 48 B per triangle test + 64 B per hit over
-            # the reference median tree -- a measure of work, served from L1/L2, not HBM bytes
+                    "frac = achieved / 8 TB/s (the HBM fraction).  `bound` names the binding resource measured "
+                    "(binding_resource): the scene is cache-resident, and each wave is bound by its own dependent "
+                    "chain (node fetch, box test, stack pop) at 4 waves per SIMD (wave_cycles; DESIGN.md §4-5)",
+            # SURVEY §8d canonical work: 64 B per 2-wide node + 48 B per triangle test + 64 B per hit,
+            # counted over the REFERENCE median-split tree (the canonical 2-wide walk), not over the
+            # timed device tree -- a measure of work, served from L1/L2/LDS, not HBM bytes
             "work_bytes_per_frame": int(work_bytes_frame),
+            "work_bytes_tree": "reference median-split tree (mybvh.cpp:375-539; SURVEY §8d canonical 2-wide walk), "
+                               "not the timed device tree",
             "work_rate_GBps": round(work_bytes_frame * frames_per_launch / kernel_s / 1e9, 1),
             "l1_roof": {"peak": round(L1_PEAK_GBPS, 1), "unit": "GB/s",
                         "fetch_bytes_per_frame": int(fetch_bytes_frame),
                         "achieved": round(fetch_bytes_frame * frames_per_launch / kernel_s / 1e9, 1),
                         "frac": round(fetch_bytes_frame * frames_per_launch / kernel_s / 1e9 / L1_PEAK_GBPS, 4),
                         "td_busy_frac": pmc.get("td_busy_frac") if pmc else None,
-                        "def": "128*wide_node_visits + 80*tri_tests + 96*closest_hits (production kernel) / "
-                               "(64 B/clk x 256 CUs x 2.4 GHz)"},
+                        "def": "128*wide_node_visits + 80*tri_tests + 96*closest_hits (production kernel's "
+                               "4-wide diagnostic variant) / (64 B/clk x 256 CUs x 2.4 GHz)",
+                        "peak_source": L1_PEAK_SOURCE},
             "wave_cycles": pmc_wave_mix(workload_key(a, n), frames_per_launch),
             "valu_roof": pmc_valu_roof(workload_key(a, n), frames_per_launch, kernel_s / frames_per_launch),
         })
+        roof["bound"], roof["bound_basis"] = binding_resource(roof)
         out = {
             "metric": f"Mrays/sec (primary+shadow+reflect), {workload_label(a, host.triangle_count)}",
             "value": round(mrays, 2),
@@ -459,6 +600,7 @@ def main():
                 **({"upload_options": upload_opts} if upload_opts else {}),
             },
             "single_frame": single,
+            "multi_gpu": multi,
             "tree_records": tree_records,
             "roofline": roof,
             "cpu_baseline": None,
@@ -472,15 +614,36 @@ def main():
 
 
 def upload_options_for(a, n):
-    """rt_upload_options fields of this run: --opt FIELD=VALUE (dev A/B), and reserve_cus -- by
-    default 32 CUs per GPU left free at N > 1 (one XCD's worth: the smallest reservation beside
-    which a kernel of RCCL's gather shape ran), none on one GPU."""
+    """rt_upload_options fields of this run: --opt FIELD=VALUE (dev A/B), and --reserve-cus (default
+    0 at any N: reserving 32 CUs slows the render by ~12 %, r04e_cumask.txt, and what it buys at
+    N > 1 -- the gather beside the next launch -- is measured by the multi_gpu.reserve_cus_ab
+    record of every N > 1 run, not assumed)."""
     opts = {k: (float(v) if "." in v else int(v)) for k, v in (o.split("=", 1) for o in a.opt)}
-    if "reserve_cus" not in opts:
-        r = a.reserve_cus if a.reserve_cus >= -1 else (32 if n > 1 else 0)
-        if r:
-            opts["reserve_cus"] = r
+    if "reserve_cus" not in opts and a.reserve_cus > 0:
+        opts["reserve_cus"] = a.reserve_cus
     return opts
+
+
+def binding_resource(roof):
+    """(bound, basis) from the measured fractions in a roofline record: HBM (roof.frac), the
+    vector-L1 data path (l1_roof.frac: useful fetch bytes / data-return peak) and VALU issue
+    (valu_roof.frac).  The largest fraction names the bound when it reaches BOUND_FRAC; else no
+    throughput roof binds and the kernel is latency-bound (per-wave dependent chains, wave_cycles).
+    TD busy is not used: it counts cycles the TD holds requests waiting on L2."""
+    fr = {"hbm": roof.get("frac"), "l1": (roof.get("l1_roof") or {}).get("frac"),
+          "valu": (roof.get("valu_roof") or {}).get("frac")}
+    known = {k: v for k, v in fr.items() if v is not None}
+    basis = {f"{k}_frac": v for k, v in fr.items()}
+    wc = roof.get("wave_cycles")
+    if wc:
+        basis["wave_mem_wait_frac"] = wc.get("mem_wait_frac")
+        basis["wave_issue_frac"] = wc.get("issue_frac")
+    basis["rule"] = f"largest measured fraction >= {BOUND_FRAC} names the roof, else latency"
+    if known:
+        k, v = max(known.items(), key=lambda kv: kv[1])
+        if v >= BOUND_FRAC:
+            return k, basis
+    return "latency", basis
 
 
 def tree_record(host, dev, a, upload_opts, tree, cams, F, fbuf, stream, rays_launch, timed_region):

@@ -220,11 +220,13 @@ typedef struct rt_upload_options {
                             persistent grid): > 0 = the launches run on an internal stream
                             whose CU mask clears the first reserve_cus CUs, the grid sized to the rest
                             (32 = one XCD's worth: the smallest reservation a 256-VGPR kernel was
-                            measured to run beside); 0 = none (default; rt_multi_create: 32 per GPU at
-                            N > 1); -1 = none */
+                            measured to run beside a stand-in of RCCL's kernel shape); 0 = none (default,
+                            also in rt_multi_create: the reservation slows the render by ~12 % and
+                            its gain at N > 1 is unmeasured; bench.py times both at N > 1); -1 = none */
   int order_window;      /* one-frame cost order (RT_FLAG_COST_ORDER, the default on one stream): a tile sorts by
                             the largest recorded cost within +-order_window tiles of its row; 0 = by size (4,
-                            exact costs for hierarchies from 2^18 device records on; default), -1 = exact */
+                            exact costs for hierarchies from 2^18 device records on, whatever stack_ring forces;
+                            default), -1 = exact */
   int reserved_[6];
 } rt_upload_options;
 

@@ -49,6 +49,11 @@ const rt_raw_scene* rt_host_raw(const rt_host_scene* s);
  * Idempotent.  Returns the build time in *seconds if non-NULL. */
 int rt_host_prepare(rt_host_scene* s, double* seconds);
 
+/* rt_host_prepare with the median-split builder's thread count: 0 = the CPUs this process may
+ * use (affinity mask, capped by a cgroup CPU quota; the rt_host_prepare default), else at most 64.
+ * The tree and the slot permutation do not depend on it.  The library reads no environment. */
+int rt_host_prepare_ex(rt_host_scene* s, int build_threads, double* seconds);
+
 /* Valid after rt_host_prepare. */
 const rt_scene_soa* rt_host_soa(const rt_host_scene* s);
 const rt_bvh_soa* rt_host_bvh(const rt_host_scene* s);

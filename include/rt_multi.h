@@ -27,9 +27,9 @@ extern "C" {
 typedef struct rt_multi rt_multi;   /* opaque: scenes, communicators, streams, stripe buffers */
 
 /* Uploads the scene to devices[0..n_devices) and creates one RCCL communicator per device.
- * n_devices >= 1; device ids must be distinct (RCCL allows one rank per GPU).  With n_devices > 1
- * the render launches leave 32 CUs per GPU free for the gathers (rt_upload_options.reserve_cus,
- * unless opt sets it: -1 = none). */
+ * n_devices >= 1; device ids must be distinct (RCCL allows one rank per GPU).  opt's reserve_cus
+ * (default 0) applies per GPU: 32 leaves one XCD's worth of CUs free for the gathers of the
+ * previous batch. */
 int rt_multi_create(const rt_scene_soa* soa, const rt_bvh_soa* bvh, const int* devices, int n_devices,
                     const rt_upload_options* opt, rt_multi** out);
 

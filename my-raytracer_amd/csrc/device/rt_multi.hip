@@ -156,8 +156,6 @@ void rt_multi_free(rt_multi* m) {
   delete m;
 }
 
-constexpr int kReserveCus = 32;   // one XCD's worth of an MI355X
-
 int rt_multi_create(const rt_scene_soa* soa, const rt_bvh_soa* bvh, const int* devices, int n_devices,
                     const rt_upload_options* opt, rt_multi** out) {
   if (!out || !devices || n_devices < 1) return fail(RT_ERR_INVALID, "rt_multi_create: bad argument");
@@ -169,14 +167,12 @@ int rt_multi_create(const rt_scene_soa* soa, const rt_bvh_soa* bvh, const int* d
   m->n = n_devices;
   m->devices.assign(devices, devices + n_devices);
   m->scenes.assign(n_devices, nullptr);
-  // N > 1: each GPU's render launches leave kReserveCus CUs free, so the RCCL gather of one batch
-  // runs beside the next batch's persistent kernel instead of waiting for its end (a 256-VGPR kernel
-  // fits beside the grid only with a whole XCD's worth free: DESIGN.md §8);
-  // the caller's reserve_cus wins when set (-1: none)
+  // reserve_cus is the caller's (default 0): leaving 32 CUs (one XCD's worth) free lets an RCCL gather run
+  // beside the next batch's persistent kernel, but costs ~12 % of the render and its
+  // gain is unmeasured at N > 1, so it is opt-in (bench.py records both settings at N > 1)
   rt_upload_options o;
   if (opt) o = *opt;
   else rt_upload_options_init(&o);
-  if (n_devices > 1 && o.reserve_cus == 0) o.reserve_cus = kReserveCus;
   if (rt_scene_upload_multi(soa, bvh, devices, n_devices, &o, m->scenes.data()) != RT_OK) {
     const std::string e = rt_last_error();
     rt_multi_free(m);

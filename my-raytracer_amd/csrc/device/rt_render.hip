@@ -1183,8 +1183,9 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
       // sort (any visit order finds the same occluded / not-occluded answer): office +3.6 %
       // batched, +2.3 % one frame; config 4 +3.2 % one frame, -1.1 % batched; testing the hit bits
       // instead of the keys (which then serve only the sorted path): office +2.1 % / +2.0 % more
-      // (A/B)
-      const bool w_any = wballot(!anyhit && cur != kDone) == 0;   // wave-uniform
+      // (A/B).  The diagnostic (STATS) variants sort every wave: their node and
+      // triangle counts then follow each lane's own distance order, not the mix of rays a wave holds
+      const bool w_any = !STATS && wballot(!anyhit && cur != kDone) == 0;   // wave-uniform
       while ((wballot(cur != kDone) | wballot(pleaf != kDone)) != 0) {
         if (++rounds > kTravGuard) {   // watchdog: abandon the round (results void, launch flagged)
           guard_trip();
@@ -2142,6 +2143,7 @@ struct rt_scene {
   int n_cu = 0;
   int blocks_per_cu[kNumVariants] = {};
   bool deep = false;            // launches use the 16-entry ring variant (deep hierarchy)
+  bool big = false;             // >= 2^18 device records, whatever ring rt_upload_options.stack_ring forced
   int n_top_v[kNumVariants] = {};   // treelet nodes of each kernel variant (by its stack ring)
   GNode4* d_nodes4 = nullptr;
   int n_gnodes4 = 0;
@@ -2173,7 +2175,7 @@ struct rt_scene {
   hipEvent_t maps_ev = nullptr;
   double build_s = 0.0, copy_s = 0.0;   // rt_scene_upload_seconds
   // rt_upload_options.reserve_cus: launches run on internal streams whose CU mask leaves that many
-  // CUs free, one per caller stream (at most kMaskedStreams, then shared round robin)
+  // CUs free, one per caller stream (at most kMaskedStreams; further callers share slot hash % 4)
   int reserve_cus = 0;
   int order_window = 0;   // rt_upload_options.order_window (0: by depth)
   static constexpr int kMaskedStreams = 4;
@@ -2257,8 +2259,9 @@ int upload_image(const SceneImage& I, const rt_upload_options& opt, int device, 
   // deep hierarchies (half a million device records and more: random-triangle soups of ~1 M and
   // up spill an 8-entry ring on every other ray, the office proxy on 1 in 130) render with the
   // 16-entry ring and the 9-node treelet that fits beside it (A/B)
-  sc->deep = I.tris.size() >= (size_t)(1u << 18);   // device records (office 77 k prefers 8, 500 k random 16)
-  if (opt.stack_ring != 0) sc->deep = opt.stack_ring >= 16;   // forced ring size
+  sc->big = I.tris.size() >= (size_t)(1u << 18);   // device records (office 77 k prefers 8, 500 k random 16)
+  sc->deep = sc->big;
+  if (opt.stack_ring != 0) sc->deep = opt.stack_ring >= 16;   // forced ring size (the order window keeps `big`)
   for (int v = 0; v < kNumVariants; ++v) {
     int& nt = sc->n_top_v[v];
     nt = top_nodes_for(sc->stack_words, variant_ring(v), sc->n_gnodes4);
@@ -2471,16 +2474,29 @@ int read_counters(const LaunchCtx& C, unsigned long long* c) {
 // (one XCD's worth); 8 or 16 CUs, or 32 spread over the mask, leave it waiting for the grid's end
 // (DESIGN.md §8).
 int masked_stream(rt_scene* sc, hipStream_t caller, hipStream_t* out) {
-  for (int i = 0; i < sc->n_masked && i < rt_scene::kMaskedStreams; ++i)
+  for (int i = 0; i < sc->n_masked; ++i)
     if (sc->masked_for[i] == caller) { *out = sc->masked[i]; return RT_OK; }
-  if (sc->n_masked >= rt_scene::kMaskedStreams) {   // more caller streams than masked ones: share
-    *out = sc->masked[(sc->n_masked++) % rt_scene::kMaskedStreams];
+  if (sc->n_masked >= rt_scene::kMaskedStreams) {
+    // more caller streams than masked ones: a further caller always shares the same slot (its
+    // handle hashed), so its launches stay in order on one internal stream
+    const uintptr_t h = reinterpret_cast<uintptr_t>(caller);
+    *out = sc->masked[(size_t)((h >> 4) ^ (h >> 12)) % rt_scene::kMaskedStreams];
     return RT_OK;
   }
   std::vector<uint32_t> mask((size_t)(sc->n_cu + 31) / 32, 0u);
   for (int c = sc->reserve_cus; c < sc->n_cu; ++c) mask[(size_t)c / 32] |= 1u << (c % 32);
   hipStream_t s = nullptr;
-  HIP_TRY(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size() * 32u, mask.data()));
+  // cuMaskSize counts uint32 words of the mask (as hipExtStreamGetCUMask's does)
+  HIP_TRY(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
+  {   // read the mask back: the stream must leave exactly the first reserve_cus CUs free
+    std::vector<uint32_t> got(mask.size(), 0u);
+    const hipError_t e = hipExtStreamGetCUMask(s, (uint32_t)got.size(), got.data());
+    if (e != hipSuccess || got != mask) {
+      (void)hipStreamDestroy(s);
+      return fail(RT_ERR_HIP, e != hipSuccess ? "hipExtStreamGetCUMask failed"
+                                              : "reserve_cus: the CU-masked stream did not take the requested mask");
+    }
+  }
   sc->masked[sc->n_masked] = s;
   sc->masked_for[sc->n_masked] = caller;
   sc->n_masked++;
@@ -2662,7 +2678,7 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
       if ((n_pos + kGroups - 1) / kGroups <= kOrderMaxRange) {   // the drain jobs: next order, next map cleared
         P.order_src = q >= 1 ? sc->d_cost[(q + 2) % 3] : nullptr;
         P.order_dilate = sc->order_window > 0 ? sc->order_window : sc->order_window < 0 ? 0
-                         : sc->deep ? 0 : kOrderDilate;
+                         : sc->big ? 0 : kOrderDilate;
         P.next_order = sc->d_order[(q + 1) % 2];
         P.zero_map = sc->d_cost[(q + 1) % 3];
         P.n_pos = n_pos;

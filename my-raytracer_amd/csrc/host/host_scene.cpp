@@ -314,23 +314,30 @@ void build_subtree(BuildCtx& cx, std::vector<FragNode>& arena, int root) {
   }
 }
 
-int build_threads() {
-  const char* e = std::getenv("RT_BUILD_THREADS");
-  int t = e ? std::atoi(e) : 0;
+// Builder threads: `requested` when > 0, else the CPUs this process may run on -- its affinity
+// mask, capped by a cgroup v2 CPU quota (a GPU box's job may use only its share of the node).
+// The library reads nothing from the environment (rt_host_prepare_ex).
+int build_threads(int requested) {
+  int t = requested;
   if (t <= 0) {
-    const char* o = std::getenv("OMP_NUM_THREADS");
-    t = o ? std::atoi(o) : 0;
-  }
-  if (t <= 0) {   // the CPUs this process may run on (affinity mask), not the whole node
     cpu_set_t set;
     t = sched_getaffinity(0, sizeof set, &set) == 0 ? CPU_COUNT(&set) : (int)std::thread::hardware_concurrency();
+    if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+      char q[32] = {0};
+      long long per = 0;
+      if (std::fscanf(f, "%31s %lld", q, &per) == 2 && std::strcmp(q, "max") != 0 && per > 0) {
+        const long long quota = std::atoll(q);
+        if (quota > 0) t = (int)std::min<long long>(t, std::max(1LL, quota / per));
+      }
+      std::fclose(f);
+    }
   }
   return std::max(1, std::min(t, 64));
 }
 
 }  // namespace
 
-void build_bvh_soa(SoA& s, BvhSoA& b) {
+void build_bvh_soa(SoA& s, BvhSoA& b, int requested_threads) {
   b = BvhSoA();
   const long long N = s.n_vertex_idx / 3;
   if (N <= 0) return;
@@ -343,7 +350,7 @@ void build_bvh_soa(SoA& s, BvhSoA& b) {
   }
   // threads = 2^par_levels; small builds stay sequential
   int levels = 0;
-  const int threads = build_threads();
+  const int threads = build_threads(requested_threads);
   while ((1 << (levels + 1)) <= threads) ++levels;
   if (N < 200000) levels = 0;
   BuildCtx cx{s, cent, levels + 1};   // root depth is 1: split in parallel while depth <= levels
@@ -415,7 +422,7 @@ void derive_camera(const rt_camera_def& def, int width, int height, rt_camera& o
   out.height = height;
 }
 
-void HostScene::prepare() {
+void HostScene::prepare(int threads) {
   if (prepared) return;
   for (auto& m : meshes) {
     if (m.draw_mode != RT_DRAW_FLAT && m.draw_mode != RT_DRAW_PHONG)
@@ -423,7 +430,7 @@ void HostScene::prepare() {
     m.compute_normals();
   }
   build_data(*this, soa);
-  build_bvh_soa(soa, bvh);
+  build_bvh_soa(soa, bvh, threads);
   rt_scene_soa& v = soa_view;
   std::memset(&v, 0, sizeof v);
   v.n_meshes = soa.n_meshes;
@@ -512,11 +519,14 @@ int rt_host_generate(const char* kind, const rt_gen_params* params, rt_host_scen
 
 const rt_raw_scene* rt_host_raw(const rt_host_scene* s) { return s ? &s->scene.raw : nullptr; }
 
-int rt_host_prepare(rt_host_scene* s, double* seconds) {
+int rt_host_prepare(rt_host_scene* s, double* seconds) { return rt_host_prepare_ex(s, 0, seconds); }
+
+int rt_host_prepare_ex(rt_host_scene* s, int build_threads, double* seconds) {
   if (!s) return host_fail("rt_host_prepare: null scene");
+  if (build_threads < 0) return host_fail("rt_host_prepare_ex: build_threads must be >= 0");
   try {
     const auto t0 = std::chrono::steady_clock::now();
-    s->scene.prepare();
+    s->scene.prepare(build_threads);
     const auto t1 = std::chrono::steady_clock::now();
     if (seconds) *seconds = std::chrono::duration<double>(t1 - t0).count();
     return RT_OK;

@@ -81,13 +81,13 @@ struct HostScene {
   rt_bvh_soa bvh_view{};
 
   void refresh_raw();              // rebuild the rt_raw_scene view
-  void prepare();                  // compute_normals + build_Data + initSoA
+  void prepare(int build_threads = 0);   // compute_normals + build_Data + initSoA (0 threads: usable CPUs)
   long long triangle_count() const;
 };
 
 // Steps of Raytracer::init_cuda (mytracer.cpp:54-60), restated.
 void build_data(const HostScene& scene, SoA& soa);       // mytracer.cpp:166-296
-void build_bvh_soa(SoA& soa, BvhSoA& bvh);               // mybvh.cpp:375-539
+void build_bvh_soa(SoA& soa, BvhSoA& bvh, int threads = 0);   // mybvh.cpp:375-539
 void derive_camera(const rt_camera_def& def, int width, int height, rt_camera& out);
 
 // loader.cpp

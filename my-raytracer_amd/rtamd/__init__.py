@@ -161,9 +161,10 @@ class HostScene:
         except Exception:
             pass
 
-    def prepare(self):
+    def prepare(self, build_threads=0):
+        """compute_normals + build_Data + BVH::initSoA; build_threads 0 = the usable CPUs."""
         secs = C.c_double(0.0)
-        _check_host(host_lib().rt_host_prepare(self.handle, C.byref(secs)), "prepare")
+        _check_host(host_lib().rt_host_prepare_ex(self.handle, int(build_threads), C.byref(secs)), "prepare")
         return secs.value
 
     @property

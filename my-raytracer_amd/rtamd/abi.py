@@ -194,6 +194,7 @@ HOST_SYMBOLS = {
     "rt_host_generate": (C.c_int, [C.c_char_p, C.POINTER(GenParams), C.POINTER(C.c_void_p)]),
     "rt_host_raw": (C.POINTER(RawScene), [C.c_void_p]),
     "rt_host_prepare": (C.c_int, [C.c_void_p, C.POINTER(C.c_double)]),
+    "rt_host_prepare_ex": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_double)]),
     "rt_host_soa": (C.POINTER(SceneSoA), [C.c_void_p]),
     "rt_host_bvh": (C.POINTER(BvhSoA), [C.c_void_p]),
     "rt_host_camera": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(Camera)]),

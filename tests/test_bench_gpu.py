@@ -50,7 +50,10 @@ def test_bench_json_contract_and_saved_frame(tmp_path, frames):
     assert d["n_gpus"] == 1 and d["steps"] == 8 and d["value"] > 0
     assert d["config"]["frames_per_launch"] == frames
     rf = d["roofline"]
-    assert rf["bound"] == "hbm" and rf["peak"] == 8000.0 and rf["kernel_ms_avg"] > 0
+    assert rf["bound"] in ("hbm", "l1", "valu", "latency") and rf["peak"] == 8000.0 and rf["kernel_ms_avg"] > 0
+    assert rf["bound_basis"]["rule"] and "reference median-split" in rf["work_bytes_tree"]
+    assert "l1_micro" in rf["l1_roof"]["peak_source"]
+    assert d["multi_gpu"] is None
     assert rf["frac"] is None or 0.0 < rf["frac"] <= 1.0
     sf = d["single_frame"]
     assert sf["frames"] == min(16, frames) and sf["ms_per_frame"] > 0 and sf["value"] > 0
@@ -98,6 +101,27 @@ def test_bench_two_ranks_rehearsal(tmp_path):
     assert d["config"]["rays_per_frame"] == rays
 
 
+def test_bench_gpus_two_without_launcher(tmp_path):
+    # `bench.py --gpus 2` with no launcher starts its two ranks itself (before any GPU call in the
+    # parent) and prints rank 0's line with n_gpus 2; both ranks on this one GPU over gloo
+    # (RT_BENCH_DEVICE=0); the assembled frame equals the single-GPU render bit for bit
+    import os
+
+    out = tmp_path / "frame2s.npy"
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["RT_BENCH_DEVICE"] = "0"
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+                        "--steps", "16", "--warmup", "8", "--frames", "8", "--width", "320", "--height", "180",
+                        "--no-cpu-baseline", "--save", str(out)],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["n_gpus"] == 2 and d["value"] > 0
+    ref, rays = expected_frames(320, 180, 8)
+    assert np.array_equal(np.load(out), ref)
+    assert d["config"]["rays_per_frame"] == rays
+
+
 def test_bench_four_ranks_driver_shape(tmp_path):
     # the driver's command shape (--steps 20 --warmup 5, default frames per launch: 10 per rank
     # launch, two launches in flight) with 4 ranks on this one GPU over gloo: stripes of 16 rows
@@ -119,6 +143,16 @@ def test_bench_four_ranks_driver_shape(tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     d = json.loads(r.stdout.strip().splitlines()[-1])
     assert d["n_gpus"] == 4 and d["config"]["frames_per_launch"] == 10 and d["steps"] == 20
+    # the N > 1 instrumentation: render and gather time per launch (max over ranks), and the run
+    # again with 32 CUs reserved for the gather (reserve_cus 0 is the default)
+    m = d["multi_gpu"]
+    assert m["render_ms_per_launch_max"] >= m["render_ms_per_launch_rank0"] > 0
+    assert m["gather_ms_per_launch_max"] >= m["gather_ms_per_launch_rank0"] > 0
+    assert m["reserve_cus"] == 0 and m["gather_MB_per_launch_into_rank0"] > 0
+    ab = m["reserve_cus_ab"]
+    assert set(ab) == {"0", "32"} and ab["0"]["value"] == d["value"]
+    for rec in ab.values():
+        assert rec["value"] > 0 and rec["render_ms_per_launch_max"] > 0 and rec["gather_ms_per_launch_rank0"] > 0
     ref, rays = expected_frames(320, 180, 10)
     assert np.array_equal(np.load(out), ref)
     assert d["config"]["rays_per_frame"] == rays

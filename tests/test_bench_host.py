@@ -49,12 +49,62 @@ def test_metric_names_the_workload():
     assert b.workload_label(a, 59670) == "Office 3840x2160 16spp"
 
 
-def test_reserve_cus_at_n_above_one():
-    # N > 1: the render launches leave 32 CUs free for the RCCL gather; one GPU: none
+def test_reserve_cus_is_opt_in():
+    # reserving CUs for the gather costs the render ~12 % (r04e_cumask.txt) and its gain at N > 1 is
+    # measured by multi_gpu.reserve_cus_ab, so no run reserves CUs unless asked
     b = _bench()
-    a = types.SimpleNamespace(opt=[], reserve_cus=-2)
+    a = types.SimpleNamespace(opt=[], reserve_cus=0)
     assert b.upload_options_for(a, 1) == {}
-    assert b.upload_options_for(a, 8) == {"reserve_cus": 32}
-    assert b.upload_options_for(types.SimpleNamespace(opt=[], reserve_cus=0), 8) == {}
-    assert b.upload_options_for(types.SimpleNamespace(opt=["reserve_cus=4", "lds_treelet=9"], reserve_cus=-2), 8) == \
+    assert b.upload_options_for(a, 8) == {}
+    assert b.upload_options_for(types.SimpleNamespace(opt=[], reserve_cus=32), 8) == {"reserve_cus": 32}
+    assert b.upload_options_for(types.SimpleNamespace(opt=["reserve_cus=4", "lds_treelet=9"], reserve_cus=0), 8) == \
         {"reserve_cus": 4, "lds_treelet": 9}
+
+
+def test_binding_resource_vocabulary():
+    b = _bench()
+    # the office at the driver's shape (BENCH_r04): no roof near its peak -> latency-bound
+    roof = {"frac": 0.03, "l1_roof": {"frac": 0.681}, "valu_roof": {"frac": 0.498},
+            "wave_cycles": {"mem_wait_frac": 0.455, "issue_frac": 0.375}}
+    bound, basis = b.binding_resource(roof)
+    assert bound == "latency" and basis["l1_frac"] == 0.681 and basis["wave_mem_wait_frac"] == 0.455
+    assert b.binding_resource({"frac": 0.85, "l1_roof": {"frac": 0.3}})[0] == "hbm"
+    assert b.binding_resource({"frac": 0.1, "l1_roof": {"frac": 0.9}, "valu_roof": {"frac": 0.5}})[0] == "l1"
+    assert b.binding_resource({"frac": None, "l1_roof": None, "valu_roof": {"frac": 0.95}})[0] == "valu"
+    assert b.binding_resource({})[0] == "latency"
+    assert set(b.BOUND_VOCAB) == {"hbm", "l1", "valu", "latency"}
+
+
+def _launch(args, env_extra=None, timeout=240):
+    import os
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, str(ROOT / "bench.py"), *args], capture_output=True, text=True,
+                          timeout=timeout, cwd=ROOT, env=env)
+
+
+def test_gpus_n_starts_n_ranks_without_a_launcher():
+    # `python bench.py --gpus N` with no launcher (no WORLD_SIZE) starts N child ranks itself, before
+    # any GPU call; --launch-check stops them after they joined a process group of N (no GPU here)
+    import json
+    for n in (2, 3):
+        r = _launch(["--gpus", str(n), "--launch-check"])
+        assert r.returncode == 0, r.stderr[-2000:]
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        assert d["launch_check"] and d["n_gpus"] == n and d["ranks"] == list(range(n)) and d["distinct_pids"] == n
+
+
+def test_gpus_mismatch_with_launcher_fails():
+    r = _launch(["--gpus", "2", "--launch-check"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
+
+
+def test_gpus_beyond_visible_devices_fails():
+    # no launcher, more GPUs asked than visible (none in this container): exit 2 before any rank starts
+    import torch
+    if torch.cuda.device_count() >= 2:
+        return
+    r = _launch(["--gpus", "2", "--steps", "1"])
+    assert r.returncode == 2 and "GPU(s) visible" in r.stderr

@@ -823,11 +823,10 @@ def test_tree_independent_of_build_threads(tree):
     hs = rtamd.HostScene.generate("random_tris", n_triangles=300000, seed=5)
     hs.prepare()
     p = hs.render_params(192, 108, 1)
-    # traversal counts of closest-hit rays only: an any-hit wave's visit order (sorted or not)
-    # depends on which rays share the wave, which fan-out timing decides
+    # traversal counts of every ray, shadow rays included (the STATS variants visit children
+    # nearest-first in every wave, so the counts do not depend on which rays share a wave)
     q = rtamd.abi.RenderParams.from_buffer_copy(p)
     q.flags = rtamd.RT_FLAG_WIDE_STATS
-    q.n_lights = 0
     out = []
     for t in (1, 7):
         dev = rtamd.DeviceScene(hs, 0, tree=tree, build_threads=t)
@@ -994,18 +993,21 @@ def test_spatial_splits_stress_scene_bit_identical(tmp_path):
         extra = {"sbvh_leaf_max": 1} if tree == "sbvh1" else {}
         dev = rtamd.DeviceScene(hs, 0, tree="sbvh" if tree == "sbvh1" else tree, **extra)
         img, st = dev.render(p)
-        # triangle tests of closest-hit rays only (no lights): any-hit waves visit children in
-        # node order, so their test counts depend on the layout, not only on the splits
+        # triangle tests of every ray (the STATS variants sort any-hit waves too, so shadow rays'
+        # counts follow the splits, not the node layout), and of closest-hit rays alone (no lights)
         q = rtamd.abi.RenderParams.from_buffer_copy(p)
         q.flags = rtamd.RT_FLAG_WIDE_STATS
-        q.n_lights = 0
         _, wst = dev.render(q)
-        out[tree] = (img, counts(st), wst.tri_tests)
+        q.n_lights = 0
+        _, cst = dev.render(q)
+        out[tree] = (img, counts(st), wst.tri_tests, cst.tri_tests)
         dev.close()
     assert np.array_equal(out["sbvh"][0], out["reference"][0]) and out["sbvh"][1] == out["reference"][1]
     assert np.array_equal(out["sah"][0], out["reference"][0]) and out["sah"][1] == out["reference"][1]
     assert np.array_equal(out["sbvh1"][0], out["reference"][0]) and out["sbvh1"][1] == out["reference"][1]
-    assert out["sbvh1"][2] < out["sah"][2]   # the fan is split: fewer triangle tests
+    assert out["sbvh1"][2] < out["sah"][2]   # the fan is split: fewer triangle tests (all rays)
+    assert out["sbvh1"][3] < out["sah"][3]   # ... and for closest-hit rays alone
+    assert out["sbvh1"][2] - out["sbvh1"][3] < out["sah"][2] - out["sah"][3]   # ... and for shadow rays alone
     ref, cnt = pyoracle.Oracle(hs.raw, hs).render(p, pyoracle.MODE_REFERENCE)
     assert np.abs(out["sbvh"][0] - ref).max() <= TOL64
     assert out["sbvh"][1] == counts(cnt)

@@ -133,14 +133,13 @@ def test_bad_inputs_raise(tmp_path):
         rtamd.HostScene.load(bad)
 
 
-def test_parallel_builder_is_bit_identical_to_sequential(monkeypatch):
+def test_parallel_builder_is_bit_identical_to_sequential():
     # The median-split builder splits subtrees on threads and replays the reference's
     # id allocation afterwards (host_scene.cpp build_bvh_soa): same tree, same permutation.
     out = []
-    for threads in ("1", "8"):
-        monkeypatch.setenv("RT_BUILD_THREADS", threads)
+    for threads in (1, 8):
         hs = rtamd.HostScene.generate("random_tris", n_triangles=300_000, seed=7)
-        hs.prepare()
+        hs.prepare(build_threads=threads)
         out.append((hs.bvh_arrays(), hs.soa_arrays(), hs.bvh_depth, hs))
     (b1, s1, d1, _), (b8, s8, d8, _) = out
     assert d1 == d8

@@ -48,7 +48,7 @@ for name, freed in patterns.items():
             words[c // 32] |= 1 << (c % 32)
     arr = (C.c_uint32 * len(words))(*words)
     s = C.c_void_p()
-    assert hip.hipExtStreamCreateWithCUMask(C.byref(s), 32 * len(words), arr) == 0
+    assert hip.hipExtStreamCreateWithCUMask(C.byref(s), len(words), arr) == 0
     got = (C.c_uint32 * len(words))()
     hip.hipExtStreamGetCUMask(s, len(words), got)
     sa = torch.cuda.ExternalStream(s.value)
