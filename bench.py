@@ -64,7 +64,7 @@ import torch.distributed as dist
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "my-raytracer_amd"))
 import rtamd  # noqa: E402
-from rtamd.shard import HaloExchange, StripeGather, max_rows as shard_max_rows  # noqa: E402
+from rtamd.shard import HaloExchange, PeerFrames, StripeGather, max_rows as shard_max_rows  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # The CU's vector-L1 data return (TD): one 64-lane dwordx4 wave-instruction per 16 cycles =
@@ -138,6 +138,14 @@ def parse():
     ap.add_argument("--reserve-ab", choices=["auto", "on", "off"], default="auto",
                     help="N > 1: after the timed run, time the same run again with the other reserve_cus setting "
                          "(32 if the run used 0, else 0) and report both (multi_gpu.reserve_cus_ab); auto = on at N > 1")
+    ap.add_argument("--assembly", choices=["gather", "peer"], default="gather",
+                    help="N > 1 frame assembly on rank 0: gather = one RCCL gather of every launch's stripes + "
+                         "re-interleave (default); peer = every rank's render writes its stripes straight into rank "
+                         "0's frame over xGMI (RT_FLAG_GLOBAL_ROWS, IPC-mapped buffers) and one RCCL all_reduce per "
+                         "launch fences it (rtamd.shard.PeerFrames)")
+    ap.add_argument("--assembly-ab", choices=["auto", "on", "off"], default="auto",
+                    help="N > 1: after the timed run, time the same run with the other assembly and check that both "
+                         "assemble bit-identical frames (multi_gpu.assembly_ab); auto = on at N > 1 without --adaptive")
     ap.add_argument("--launch-check", action="store_true",
                     help="start the ranks (--gpus N), join a gloo process group, check its size, print one JSON line "
                          "and exit before any GPU call (a dry run of the N-rank launch)")
@@ -348,16 +356,64 @@ def main():
     gathers = [StripeGather(a.height, W, STRIPE_H, n, rank, device="cuda", frames=F, host_staged=host_staged)
                for _ in range(S)]
     image = None
+    # N > 1 assembly by peer stores (--assembly peer): rank 0's whole frames, mapped by every rank;
+    # the launches write global rows (RT_FLAG_GLOBAL_ROWS)
+    if a.adaptive and a.assembly == "peer":
+        raise SystemExit("bench.py: --assembly peer does not support --adaptive")
+    assembly = a.assembly if n > 1 else "gather"
+    peer = None
+
+    def peer_frames():
+        nonlocal peer
+        if peer is None:
+            peer = PeerFrames(a.height, W, n, rank, device="cuda", frames=F, slots=S)
+        return peer
+
+    def global_rows(c):
+        q = rtamd.abi.RenderParams.from_buffer_copy(c)
+        q.flags |= rtamd.abi.RT_FLAG_GLOBAL_ROWS
+        return q
+    cams_g = [global_rows(c) for c in cams]
 
     starts, ends, launch_frames = [], [], []
     gstarts, gends = [], []   # N > 1: HIP events around each launch's gather + re-interleave
 
     def launch(li, nf, timed, flags=0):
-        """Launch li renders nf frames (steps); their stripes are then gathered to rank 0.  A one-frame
-        launch renders view cams[li % F] (the single-frame records: consecutive frames of the orbit)."""
+        """Launch li renders nf frames (steps); their stripes are then gathered to rank 0 (or, with
+        the peer assembly, written there by the render itself and fenced).  A one-frame launch
+        renders view cams[li % F] (the single-frame records: consecutive frames of the orbit)."""
         nonlocal image
         s = streams[li % S]
         bs = [fbufs[li % S][f] for f in range(nf)]
+        if assembly == "peer":
+            outs = peer_frames().outs(li % S, nf)
+            with torch.cuda.stream(s):
+                if timed:
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(s)
+                if nf == 1:
+                    c1 = cams_g[li % len(cams_g)]
+                    if flags:
+                        c1 = rtamd.abi.RenderParams.from_buffer_copy(c1)
+                        c1.flags = flags | rtamd.abi.RT_FLAG_GLOBAL_ROWS
+                    gpu.launch(c1, outs[0], stats=False, stream=s.cuda_stream)
+                else:
+                    gpu.launch_frames(cams_g[:nf], outs, stats=False, stream=s.cuda_stream)
+                if timed:
+                    e1.record(s)
+                    starts.append(e0)
+                    ends.append(e1)
+                    launch_frames.append(nf)
+                    g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    g0.record(s)
+                peer.fence()   # the frames are whole on rank 0 once every rank's render has ended
+                if timed:
+                    g1.record(s)
+                    gstarts.append(g0)
+                    gends.append(g1)
+                img = peer.image(li % S)
+                image = img[:nf] if img is not None else None
+            return
         with torch.cuda.stream(s):
             if timed:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -445,9 +501,12 @@ def main():
                  "frames_per_launch": frames_per_launch,
                  "gather_MB_per_launch_into_rank0": round((n - 1) * frames_per_launch * rows_max * W * 3 * 4 / 1e6, 2),
                  "reserve_cus": int(upload_opts.get("reserve_cus", 0)),
+                 "assembly": assembly,
                  "def": "render = HIP events around each launch on its stream; gather = HIP events around the "
-                        "collective of its frames' stripes + rank 0's re-interleave (includes waiting for the "
-                        "slowest rank's render); means over the timed launches, then max over ranks"}
+                        "collective of its frames' stripes + rank 0's re-interleave (peer assembly: around the "
+                        "fence all_reduce) -- includes waiting for the slowest rank's render; means over the "
+                        "timed launches, then max over ranks"}
+        main_frames = last_image.clone() if rank == 0 else None   # for the assembly A/B's bit check
 
     # single-frame record: the reference's use, one frame per launch (mytracer_gpu.cu:59-81)
     # (NS consecutive views of the orbit, one per launch) in the natural tile order, then with the
@@ -484,6 +543,27 @@ def main():
     if n > 1:
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
     rays_total, rays_frame0 = float(tot[0]), float(tot[1])
+
+    # N > 1: the same run with the other frame assembly (RCCL gather <-> peer stores + fence), and
+    # the last launch's assembled frames compared bit for bit with the main run's (same views)
+    if multi is not None and (a.assembly_ab == "on" or (a.assembly_ab == "auto" and not a.adaptive)):
+        main_as = assembly
+        assembly = "peer" if main_as == "gather" else "gather"
+        el2, k2, g2 = timed_run(min(a.warmup, F))
+        (el2_max, _), (k2_max, _), (g2_max, g2_r0) = over_ranks([el2, k2, g2])
+        same = torch.tensor([1.0 if rank != 0 else float(torch.equal(image, main_frames))], dtype=torch.float64,
+                            device="cuda")
+        if n > 1:
+            dist.broadcast(same, src=0)
+        multi["assembly_ab"] = {
+            main_as: {"value": round(rays_total / elapsed / 1e6, 2), "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+                      "render_ms_per_launch_max": multi["render_ms_per_launch_max"],
+                      "gather_ms_per_launch_rank0": multi["gather_ms_per_launch_rank0"]},
+            assembly: {"value": round(rays_total / el2_max / 1e6, 2), "ms_per_step": round(el2_max / a.steps * 1e3, 4),
+                       "render_ms_per_launch_max": round(k2_max, 4), "gather_ms_per_launch_rank0": round(g2_r0, 4)},
+            "frames_identical": bool(same[0] == 1.0)}
+        assembly = main_as
+        main_frames = None
 
     # N > 1: the same run with the other reserve_cus setting (0 <-> 32 CUs left free for the
     # gather), so every N > 1 line measures what the reservation costs the render and what it
@@ -609,6 +689,9 @@ def main():
             out["cpu_baseline"] = cpu_baseline(host, params, a)
         print(json.dumps(out), flush=True)
     if n > 1:
+        dist.barrier()   # every rank's work on rank 0's frames has ended before any mapping goes
+        if peer is not None:
+            peer.close()
         dist.barrier()
         dist.destroy_process_group()
 

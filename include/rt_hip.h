@@ -113,7 +113,12 @@ enum {
                                   Launches of several frames and adaptive passes keep the natural order and
                                   record nothing; one-frame launches of more than 32768 tiles (8x8 pixels) keep
                                   the natural order */
-  RT_FLAG_NATURAL_ORDER = 64   /* one-frame launch in the natural tile order, recording no costs */
+  RT_FLAG_NATURAL_ORDER = 64,  /* one-frame launch in the natural tile order, recording no costs */
+  RT_FLAG_GLOBAL_ROWS = 128    /* the output buffer holds the whole frame (camera.height rows): the shard's rows
+                                  are written at their global positions (row y at y * width * 3), not packed.
+                                  With a peer GPU's frame buffer (rt_ipc_open) every rank writes its stripes
+                                  straight into the assembled frame over xGMI; each wave's stores are released
+                                  at system scope before it exits.  Not for the adaptive pass */
 };
 
 /* One render call.  Rows are rendered as interleaved stripes:
@@ -149,7 +154,10 @@ static inline const rt_light* rt_params_light(const rt_render_params* p, int i) 
  * primary = pixels*spp; shadow = shading points x lights with a shadowable
  * material (mytracer.cpp:589); reflection = shading points with mirror > 0
  * below max_depth (mytracer.cpp:547).  node_visits / tri_tests / hits are
- * filled only with RT_FLAG_TRAVERSAL_STATS. */
+ * filled only with RT_FLAG_TRAVERSAL_STATS (canonical 2-wide walk: exact, equal to the oracle's)
+ * or RT_FLAG_WIDE_STATS (the 4-wide production traversal, every wave sorting children: with
+ * shadow rays these vary by ~1e-5 between runs, as the postponed-leaf timing and the fan-out of
+ * shadow rays to idle lanes depend on which rays share a wave). */
 typedef struct rt_stats {
   long long primary_rays;
   long long shadow_rays;
@@ -336,6 +344,18 @@ int rt_adaptive_halo_rows(const rt_render_params* p, int* rows_out, int cap);
 /* Convenience for tests / CLI: renders into a HOST buffer (allocates a device
  * buffer internally, synchronous). */
 int rt_render_to_host(rt_scene* scene, const rt_render_params* p, void* host_out, rt_stats* stats);
+
+/* Cross-process access to a device buffer, for one process per GPU (the frame-assembly mode
+ * RT_FLAG_GLOBAL_ROWS: every rank writes its stripes straight into rank 0's frame buffer).
+ * rt_ipc_get_handle exports the device allocation that holds d_ptr (an RT_IPC_HANDLE_BYTES-byte
+ * handle, plain bytes to send to the other processes) and d_ptr's byte offset in it.  Another
+ * process maps it with rt_ipc_open, with its own `device` current (peer access over xGMI enabled
+ * as needed), and gets a pointer to the same bytes; rt_ipc_close(ptr, offset) unmaps it.  The
+ * exporting process must keep the allocation alive while it is mapped elsewhere. */
+#define RT_IPC_HANDLE_BYTES 64
+int rt_ipc_get_handle(const void* d_ptr, unsigned char* handle, unsigned long long* offset);
+int rt_ipc_open(const unsigned char* handle, unsigned long long offset, int device, void** d_ptr);
+int rt_ipc_close(void* d_ptr, unsigned long long offset);
 
 /* Milliseconds of the last launch on this scene, measured with hipEvents
  * recorded around the kernel on its stream (valid after the stream syncs). */

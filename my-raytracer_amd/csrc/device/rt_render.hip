@@ -249,6 +249,7 @@ struct KParams {
   int row_begin, stripe_h, stripe_count, stripe_index;
   int rows;
   int tiles_x;
+  int out_global;           // RT_FLAG_GLOBAL_ROWS: pixels go to their global row of a whole-frame buffer
   int order_dilate;         // cost-ordered launches: cost window half-width along a tile row (order_range)
   long long n_tiles;
   // list mode (adaptive pass): list entries are frame << 25 | local pixel id; work item w = one
@@ -1758,7 +1759,10 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
           } else {
             r = stdmin(pcol.x / nn, 1.0); g = stdmin(pcol.y / nn, 1.0); b = stdmin(pcol.z / nn, 1.0);
           }
-          const size_t o = 3 * ((size_t)lrow * P.W + px);
+          // RT_FLAG_GLOBAL_ROWS: the row's place in the whole frame (the buffer may be another GPU's,
+          // mapped over xGMI: the shard's pixels land in the assembled frame as they finish)
+          const int orow = P.out_global ? (P.stripe_count == 1 ? P.row_begin + lrow : stripe_row(P, lrow)) : lrow;
+          const size_t o = 3 * ((size_t)orow * P.W + px);
           // nontemporal (evict-first): the frame is written once and never read here, so its lines
           // should not push the path-state lines out of L2 (office: HBM writes 50.9 -> 45.5 MB per
           // frame, time unchanged; profiles/r03/write_traffic_r03.json)
@@ -1822,6 +1826,9 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
     wl[2] = __builtin_amdgcn_s_memrealtime();
     wl[3] = w_pixels;
   }
+  // RT_FLAG_GLOBAL_ROWS into a peer GPU's frame: this wave's image stores are written back to
+  // memory before it exits (system-scope release), so they are there when the launch ends
+  if (P.out_global) __threadfence_system();
   // ---------------- counters: one atomic per wave and counter ----------------
   const unsigned long long s0 = wave_sum(c_primary), s1 = wave_sum(c_shadow), s2 = wave_sum(c_refl);
   unsigned long long s3 = 0, s4 = 0, s5 = 0;
@@ -2605,6 +2612,8 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   P.stripe_count = scount;
   P.stripe_index = p->stripe_index;
   P.rows = rows;
+  P.out_global = (p->flags & RT_FLAG_GLOBAL_ROWS) ? 1 : 0;
+  if (P.out_global && list) return fail(RT_ERR_INVALID, "RT_FLAG_GLOBAL_ROWS is not supported by the adaptive pass");
   P.tiles_x = (P.W + 7) / 8;
   P.nsamp = p->spp_n * p->spp_n;
   P.frame_tiles = list ? (list_cap * P.nsamp + 63) / 64 : (long long)P.tiles_x * ((rows + 7) / 8);
@@ -3079,6 +3088,37 @@ long long rt_debug_wave_log(rt_scene* sc, unsigned long long* out, long long n) 
   HIP_TRY(hipMemcpy(out, sc->ctx[sc->last_ctx].d_wavelog, (size_t)words * sizeof(unsigned long long),
                     hipMemcpyDeviceToHost));
   return words;
+}
+
+int rt_ipc_get_handle(const void* d_ptr, unsigned char* handle, unsigned long long* offset) {
+  if (!d_ptr || !handle || !offset) return fail(RT_ERR_INVALID, "rt_ipc_get_handle: null argument");
+  static_assert(sizeof(hipIpcMemHandle_t) == RT_IPC_HANDLE_BYTES, "IPC handle size");
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  HIP_TRY(hipMemGetAddressRange(&base, &size, const_cast<void*>(d_ptr)));
+  hipIpcMemHandle_t h;
+  HIP_TRY(hipIpcGetMemHandle(&h, base));
+  std::memcpy(handle, &h, sizeof h);
+  *offset = (unsigned long long)(reinterpret_cast<const char*>(d_ptr) - reinterpret_cast<const char*>(base));
+  return RT_OK;
+}
+
+int rt_ipc_open(const unsigned char* handle, unsigned long long offset, int device, void** d_ptr) {
+  if (!handle || !d_ptr) return fail(RT_ERR_INVALID, "rt_ipc_open: null argument");
+  *d_ptr = nullptr;
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle, sizeof h);
+  HIP_TRY(hipSetDevice(device));
+  void* base = nullptr;
+  HIP_TRY(hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess));
+  *d_ptr = reinterpret_cast<char*>(base) + offset;
+  return RT_OK;
+}
+
+int rt_ipc_close(void* d_ptr, unsigned long long offset) {
+  if (!d_ptr) return fail(RT_ERR_INVALID, "rt_ipc_close: null pointer");
+  HIP_TRY(hipIpcCloseMemHandle(reinterpret_cast<char*>(d_ptr) - offset));
+  return RT_OK;
 }
 
 int rt_last_kernel_ms(rt_scene* sc, float* ms) {

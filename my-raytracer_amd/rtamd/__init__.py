@@ -409,6 +409,29 @@ class DeviceScene:
         return ms.value
 
 
+def ipc_handle(d_ptr):
+    """(handle bytes, offset) exporting the device allocation that holds d_ptr to other
+    processes (rt_ipc_get_handle)."""
+    h = C.create_string_buffer(abi.RT_IPC_HANDLE_BYTES)
+    off = C.c_ulonglong(0)
+    _check_hip(hip_lib().rt_ipc_get_handle(C.c_void_p(d_ptr), h, C.byref(off)), "rt_ipc_get_handle")
+    return h.raw, off.value
+
+
+def ipc_open(handle, offset, device):
+    """Device pointer in this process (device `device` current) to the bytes another process
+    exported with ipc_handle (rt_ipc_open)."""
+    if len(handle) != abi.RT_IPC_HANDLE_BYTES:
+        raise ValueError("IPC handle must be RT_IPC_HANDLE_BYTES bytes")
+    p = C.c_void_p(0)
+    _check_hip(hip_lib().rt_ipc_open(handle, C.c_ulonglong(offset), int(device), C.byref(p)), "rt_ipc_open")
+    return int(p.value)
+
+
+def ipc_close(d_ptr, offset):
+    _check_hip(hip_lib().rt_ipc_close(C.c_void_p(d_ptr), C.c_ulonglong(offset)), "rt_ipc_close")
+
+
 def rows_in_shard(params):
     return int(hip_lib().rt_rows_in_shard(C.byref(params)))
 

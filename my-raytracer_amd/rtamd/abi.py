@@ -25,6 +25,8 @@ RT_FLAG_TILE_COST = 8
 RT_FLAG_TILE_COST_TIME = 16
 RT_FLAG_COST_ORDER = 32
 RT_FLAG_NATURAL_ORDER = 64
+RT_FLAG_GLOBAL_ROWS = 128
+RT_IPC_HANDLE_BYTES = 64
 
 
 class Material(C.Structure):
@@ -177,6 +179,9 @@ HIP_SYMBOLS = {
     "rt_adaptive_halo_rows": (C.c_int, [C.POINTER(RenderParams), C.POINTER(C.c_int), C.c_int]),
     "rt_render_to_host": (C.c_int, [C.c_void_p, C.POINTER(RenderParams), C.c_void_p, C.POINTER(Stats)]),
     "rt_last_kernel_ms": (C.c_int, [C.c_void_p, C.POINTER(C.c_float)]),
+    "rt_ipc_get_handle": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(C.c_ulonglong)]),
+    "rt_ipc_open": (C.c_int, [C.c_char_p, C.c_ulonglong, C.c_int, C.POINTER(C.c_void_p)]),
+    "rt_ipc_close": (C.c_int, [C.c_void_p, C.c_ulonglong]),
     "rt_debug_counters": (C.c_int, [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]),
     "rt_debug_wave_log": (C.c_longlong, [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_longlong]),
     "rt_debug_timeline": (C.c_longlong, [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_longlong]),

@@ -66,6 +66,60 @@ class StripeGather:
         return image
 
 
+class PeerFrames:
+    """Frame assembly without a gather (RT_FLAG_GLOBAL_ROWS): rank 0 owns `slots` sets of whole
+    frames [frames, H, W, C]; every other rank maps them into its address space (rt_ipc_open: IPC
+    handles sent once with broadcast_object_list; peer access over xGMI) and its render launches
+    write their stripes straight to their global rows there, as pixels finish -- the transfer
+    overlaps the render, and there is neither a copy nor a re-interleave.  A launch's frames are
+    complete on rank 0 after fence(): a one-element all_reduce on the launch stream of every rank
+    (RCCL with "nccl"), which starts after that rank's render in stream order, so rank 0's stream
+    passes it only when every rank's render has ended (its waves release their image stores at
+    system scope before they exit).  With frames == 0 the buffers are single images [H, W, C]."""
+
+    def __init__(self, height, width, n, rank, device, frames=0, slots=1, dtype=torch.float32, channels=3):
+        from . import ipc_handle, ipc_open   # librt_hip (lazy: importing this module needs no GPU)
+        self.n, self.rank, self.slots = n, rank, slots
+        lead = (frames,) if frames else ()
+        self.frame_elems = height * width * channels
+        self.elem = torch.empty((), dtype=dtype).element_size()
+        self.images = [torch.zeros(lead + (height, width, channels), dtype=dtype, device=device)
+                       for _ in range(slots)] if rank == 0 else None
+        handles = [[ipc_handle(im.data_ptr()) for im in self.images]] if rank == 0 else [None]
+        if n > 1:
+            dist.broadcast_object_list(handles, src=0)
+        dev = torch.device(device).index if torch.device(device).index is not None else torch.cuda.current_device()
+        self._opened = []
+        if rank == 0:
+            self.base = [im.data_ptr() for im in self.images]
+        else:
+            self.base = []
+            for h, off in handles[0]:
+                ptr = ipc_open(h, off, dev)
+                self._opened.append((ptr, off))
+                self.base.append(ptr)
+        self.flag = torch.zeros(1, dtype=torch.float32, device=device)
+
+    def outs(self, slot, nf):
+        """Device pointers (valid in this process) of frames 0..nf of buffer set `slot`."""
+        step = self.frame_elems * self.elem
+        return [self.base[slot] + f * step for f in range(nf)]
+
+    def fence(self):
+        """On the current stream: every rank's work enqueued so far on its launch stream has ended."""
+        if self.n > 1:
+            dist.all_reduce(self.flag)
+
+    def image(self, slot):
+        return self.images[slot] if self.rank == 0 else None
+
+    def close(self):
+        from . import ipc_close
+        for ptr, off in self._opened:
+            ipc_close(ptr, off)
+        self._opened = []
+
+
 def segments(rows):
     """Runs of consecutive global rows in a shard's packed row list: [(first, last) local index]."""
     rows = np.asarray(rows)

@@ -122,6 +122,29 @@ def test_bench_gpus_two_without_launcher(tmp_path):
     assert d["config"]["rays_per_frame"] == rays
 
 
+def test_bench_peer_assembly_two_ranks(tmp_path):
+    # --assembly peer: rank 1 maps rank 0's frame buffers (IPC) and its launches write their stripes
+    # there at their global rows; here both ranks share this one GPU (gloo fences); the assembled
+    # frame equals the single-GPU render bit for bit, as does the gather A/B run's
+    import os
+
+    out = tmp_path / "framep.npy"
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["RT_BENCH_DEVICE"] = "0"
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+                        "--assembly", "peer", "--reserve-ab", "off", "--steps", "16", "--warmup", "8", "--frames", "8",
+                        "--width", "320", "--height", "180", "--no-cpu-baseline", "--save", str(out)],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    m = d["multi_gpu"]
+    assert d["n_gpus"] == 2 and m["assembly"] == "peer" and m["assembly_ab"]["frames_identical"] is True
+    assert "reserve_cus_ab" not in m
+    ref, rays = expected_frames(320, 180, 8)
+    assert np.array_equal(np.load(out), ref)
+    assert d["config"]["rays_per_frame"] == rays
+
+
 def test_bench_four_ranks_driver_shape(tmp_path):
     # the driver's command shape (--steps 20 --warmup 5, default frames per launch: 10 per rank
     # launch, two launches in flight) with 4 ranks on this one GPU over gloo: stripes of 16 rows
@@ -153,6 +176,10 @@ def test_bench_four_ranks_driver_shape(tmp_path):
     assert set(ab) == {"0", "32"} and ab["0"]["value"] == d["value"]
     for rec in ab.values():
         assert rec["value"] > 0 and rec["render_ms_per_launch_max"] > 0 and rec["gather_ms_per_launch_rank0"] > 0
+    # the other frame assembly (peer stores into rank 0's frame + a fence), bit-identical frames
+    assert m["assembly"] == "gather"
+    asm = m["assembly_ab"]
+    assert asm["frames_identical"] is True and asm["gather"]["value"] == d["value"] and asm["peer"]["value"] > 0
     ref, rays = expected_frames(320, 180, 10)
     assert np.array_equal(np.load(out), ref)
     assert d["config"]["rays_per_frame"] == rays
