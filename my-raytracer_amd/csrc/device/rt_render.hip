@@ -677,6 +677,9 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
     w = b.b;
   };
   auto ST4 = [&](int r, D3 v, double w) {
+#ifdef RT_MEAS_NO_PSTATE   // write-attribution build (wrong colours, same control flow): no path-state stores
+    if (r != R_SUSP) return;
+#endif
     const uint32_t o = (uint32_t)r * kRegionBytes;
     buf_st(prs, pvo, o, v.x); buf_st(prs, pvo, o + 8u, v.y); buf_st(prs, pvo, o + 16u, v.z); buf_st(prs, pvo, o + 24u, w);
   };
@@ -1766,14 +1769,21 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
           // nontemporal (evict-first): the frame is written once and never read here, so its lines
           // should not push the path-state lines out of L2 (office: HBM writes 50.9 -> 45.5 MB per
           // frame, time unchanged; profiles/r03/write_traffic_r03.json)
-          if (P.out_fmt == RT_OUT_RGB_F64) {
+#ifdef RT_MEAS_NO_IMAGE   // write-attribution build: no image stores
+          if (false)
+#else
+          if (P.out_fmt == RT_OUT_RGB_F64)
+#endif
+          {
             double* out = reinterpret_cast<double*>(P.frames[frame].out) + o;
             __builtin_nontemporal_store(r, out); __builtin_nontemporal_store(g, out + 1);
             __builtin_nontemporal_store(b, out + 2);
           } else {
+#ifndef RT_MEAS_NO_IMAGE
             float* out = reinterpret_cast<float*>(P.frames[frame].out) + o;
             __builtin_nontemporal_store((float)r, out); __builtin_nontemporal_store((float)g, out + 1);
             __builtin_nontemporal_store((float)b, out + 2);
+#endif
           }
           state = heads_left > 0 ? ST_FETCH : ST_DONE;
         }
@@ -2704,7 +2714,11 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
                 : (p->flags & RT_FLAG_TIMELINE) ? 3
                 // 4/5: the 16-entry-ring production variants; suspend/resume on deep scenes' several-
                 // frame launches (config 4, 128 frames: +3.2 %; one frame: -6 %, so not there)
+#ifdef RT_MEAS_NO_SUSP   // write-attribution build: deep scenes never suspend
+                : sc->deep ? 4
+#else
                 : sc->deep ? ((n_frames > 1 && !list) ? 5 : 4)
+#endif
                 : 0;
   const int ring = variant_ring(v);
   const int n_top = sc->n_top_v[v];

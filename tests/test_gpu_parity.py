@@ -1047,9 +1047,10 @@ def test_spatial_splits_stress_scene_bit_identical(tmp_path):
         _, wst = dev.render(q)
         _, wst2 = dev.render(q)
         # the 4-wide diagnostic counts depend slightly on which rays share a wave (postponed-leaf
-        # timing, fan-out of shadow rays to idle lanes): r05b saw +-2 of 246 k node visits between runs
-        assert abs(wst.node_visits - wst2.node_visits) <= 1e-4 * wst.node_visits, tree
-        assert abs(wst.tri_tests - wst2.tri_tests) <= 1e-4 * wst.tri_tests, tree
+        # timing, fan-out of shadow rays to idle lanes): between runs r05b saw 2 of 246 k node visits
+        # (sbvh), r05c 106 of 709 k (reference tree, big leaves)
+        assert abs(wst.node_visits - wst2.node_visits) <= 2e-3 * wst.node_visits, tree
+        assert abs(wst.tri_tests - wst2.tri_tests) <= 2e-3 * wst.tri_tests, tree
         q.n_lights = 0
         _, cst = dev.render(q)
         out[tree] = (img, counts(st), wst.tri_tests, cst.tri_tests)
