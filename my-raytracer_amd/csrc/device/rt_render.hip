@@ -1081,6 +1081,9 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
       uint32_t sq = 0, sqlim = kRingB;
       bool susp_now = false;   // SUSP: this lane's traversal is parked at the end of this phase
       uint32_t susp_pleaf = kDone;
+#ifdef RT_PLEAF2
+      uint32_t susp_pleaf2 = kDone;
+#endif
       if constexpr (SUSP) {
         // the parked record: {cur | postponed leaf << 32, sp | slo << 16 | shadow hit << 31 | best << 32,
         // best slot, t-limit}; the ray setup above is recomputed bit for bit from the slot
@@ -1096,6 +1099,9 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
           shadow_hit = ((w1 >> 31) & 1ull) != 0ull;
           best = (int)(uint32_t)(w1 >> 32);
           best_slot = (int)(uint32_t)__double_as_longlong(b.a);
+#ifdef RT_PLEAF2
+          susp_pleaf2 = (uint32_t)((unsigned long long)__double_as_longlong(b.a) >> 32);
+#endif
           tlim = b.b;
           hi_c = round_up_f(tlim - t_off);
         }
@@ -1236,8 +1242,16 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
           return occluded;
       };
       uint32_t pleaf = kDone;   // 4-wide: postponed leaf
+#ifdef RT_PLEAF2
+      // A/B variant: up to two postponed leaves per lane before the wave votes for the leaf phase
+      // (more leaf work per leaf-phase iteration; t-culling and occlusion found later)
+      uint32_t pleaf2 = kDone;
+#endif
       if constexpr (SUSP) {
         if (resumed) pleaf = susp_pleaf;
+#ifdef RT_PLEAF2
+        if (resumed) pleaf2 = susp_pleaf2;
+#endif
       }
 
       uint32_t rounds = 0;
@@ -1265,8 +1279,14 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
                                             ((unsigned long long)(uint32_t)best << 32);
               buf_st(prs, pvo, (uint32_t)R_SUSP * kRegionBytes, __longlong_as_double((long long)w0));
               buf_st(prs, pvo, (uint32_t)R_SUSP * kRegionBytes + 8u, __longlong_as_double((long long)w1));
+#ifdef RT_PLEAF2
+              buf_st(prs, pvo, (uint32_t)R_SUSP * kRegionBytes + 16u,
+                     __longlong_as_double((long long)((unsigned long long)(uint32_t)best_slot |
+                                                      ((unsigned long long)pleaf2 << 32))));
+#else
               buf_st(prs, pvo, (uint32_t)R_SUSP * kRegionBytes + 16u,
                      __longlong_as_double((long long)(unsigned long long)(uint32_t)best_slot));
+#endif
               buf_st(prs, pvo, (uint32_t)R_SUSP * kRegionBytes + 24u, tlim);
               susp_now = true;
             }
@@ -1396,11 +1416,24 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
           }
           }
 #undef RT_CSWAP
+#ifdef RT_PLEAF2
+          if ((cur & kLeaf) && cur != kDone) {   // first / second leaf: postpone, keep going
+            if (pleaf == kDone) {
+              pleaf = cur;
+              cur = pop();
+            } else if (pleaf2 == kDone) {
+              pleaf2 = cur;
+              cur = pop();
+            }
+          }
+          if ((wballot(pleaf2 == kDone) & wballot(cur != kDone)) == 0) break;   // every lane holds two leaves or is done
+#else
           if ((cur & kLeaf) && cur != kDone && pleaf == kDone) {   // first leaf: postpone, keep going
             pleaf = cur;
             cur = pop();
           }
           if ((wballot(pleaf == kDone) & wballot(cur != kDone)) == 0) break;   // every lane holds a leaf (one mask per compare)
+#endif
         }
         }
         // leaves: 2-wide -- the leaf the lane stopped at; 4-wide -- the postponed leaf, then
@@ -1420,10 +1453,19 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
             if (test_leaf(pleaf)) {   // any-hit: occluded, the ray is finished
               cur = kDone;
               pleaf = kDone;
+#ifdef RT_PLEAF2
+              pleaf2 = kDone;
+#endif
               break;
             }
+#ifdef RT_PLEAF2
+            pleaf = pleaf2;
+            pleaf2 = kDone;
+            if (pleaf == kDone && (cur & kLeaf) && cur != kDone) {
+#else
             pleaf = kDone;
             if ((cur & kLeaf) && cur != kDone) {
+#endif
               pleaf = cur;
               cur = pop();
             }
