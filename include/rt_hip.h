@@ -111,7 +111,7 @@ enum {
                                   launch); launches on another stream keep the natural order unless they set
                                   this flag, which then makes them wait for the last ordered launch.
                                   Launches of several frames and adaptive passes keep the natural order and
-                                  record nothing; one-frame launches of more than 32768 tiles (8x8 pixels) keep
+                                  record nothing; one-frame launches of more than 32768 tiles (rt_tile_shape) keep
                                   the natural order */
   RT_FLAG_NATURAL_ORDER = 64,  /* one-frame launch in the natural tile order, recording no costs */
   RT_FLAG_GLOBAL_ROWS = 128    /* the output buffer holds the whole frame (camera.height rows): the shard's rows
@@ -395,9 +395,14 @@ int rt_debug_blocks_per_cu(rt_scene* scene, int variant);
  * words copied. */
 long long rt_debug_timeline(rt_scene* scene, unsigned long long* out, long long n);
 
+/* The render kernel's work tile: one wave's 64 pixels, *tile_w x *tile_h (16 x 4: a tile row of
+ * fp32 RGB is 192 B, whole 64-B write units of the image).  Tile positions of the diagnostics
+ * below are ty * ceil(width / tile_w) + tx over the shard's ceil(rows / tile_h) tile rows. */
+int rt_tile_shape(int* tile_w, int* tile_h);
+
 /* Diagnostics (tile-order experiments): the per-tile-position cost map of the last launch with
  * RT_FLAG_TILE_COST / RT_FLAG_TILE_COST_TIME / RT_FLAG_COST_ORDER (index ty * tiles_x + tx over the
- * shard's 8x8 tiles; per finished sample its bounces + 1, or per pixel its lifetime in 10-ns ticks;
+ * shard's tiles (rt_tile_shape); per finished sample its bounces + 1, or per pixel its lifetime in 10-ns ticks;
  * summed over the launch's frames) into out[0..n); returns the number of positions, 0 if none. */
 long long rt_debug_tile_cost(rt_scene* scene, unsigned int* out, long long n);
 /* Diagnostics: launches with exactly n tiles take linear tile order[w / 64] for work item w (a

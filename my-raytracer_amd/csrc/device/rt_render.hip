@@ -24,7 +24,7 @@
 //   * rays live in LDS slots (fp64 origin / direction / t-limit + 3 aux words
 //     holding the hit's barycentrics or the bounce normal); idle lanes are lent
 //     to owners for their extra shadow rays and reflection ray (fan-out);
-//   * work distribution: persistent workgroups pull 8x8 pixel tiles from 8
+//   * work distribution: persistent workgroups pull 16x4 pixel tiles from 8
 //     work heads on separate cache lines, one per XCD group, refilled per wave
 //     with a single atomic when >= kRefill lanes are idle; several frames per
 //     launch share the queue in band-major order (each head serves one row band
@@ -533,6 +533,19 @@ __device__ __forceinline__ TriOps load_tri(const GTri* tris, uint32_t i) {
   return T;
 }
 
+// Work tiles: one wave's 64 pixels, kTileW x kTileH.  16 x 4 (round 5): a tile row is 16 fp32
+// RGB pixels = 192 B, three whole 64-B write units of the image (rows of 1920 px are 64-B aligned),
+// where 8 x 8 tiles (round 1-4) wrote 96-B row segments that straddle them: HBM writes of the image
+// were 36.2 MB per office frame for 24.9 MB of pixels (profiles/r05/r05e_write_attrib_*); the
+// unit is also the grain of the cost order (rt_debug_tile_cost and friends).
+#ifndef RT_TILE_W
+#define RT_TILE_W 16
+#endif
+constexpr int kTileW = RT_TILE_W, kTileH = 64 / RT_TILE_W;
+constexpr int kTileWLog = kTileW == 8 ? 3 : kTileW == 16 ? 4 : kTileW == 32 ? 5 : -1;
+constexpr int kTileHLog = 6 - kTileWLog;
+static_assert(kTileWLog > 0 && kTileW * kTileH == 64, "a tile is one wave's 64 pixels (8, 16 or 32 wide)");
+
 // Path state kept in global memory between a lane's rays: per wave kRegions regions of
 // [64 lanes][4 fp64], so a lane's record of a region is ONE 32-B sector, read with two b128 and
 // written with four b64 buffer accesses at the lane offset (one VGPR) plus the region's offset
@@ -905,8 +918,8 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
             const uint32_t rem = tile - ty * row_tiles;
             frame = P.n_frames > 1 ? (int)P.div_tiles_x.div(rem) : 0;
             const int tx = (int)(rem - (uint32_t)frame * (uint32_t)P.tiles_x);
-            px = tx * 8 + (j & 7);
-            lrow = (int)ty * 8 + (j >> 3);
+            px = tx * kTileW + (j & (kTileW - 1));
+            lrow = (int)ty * kTileH + (j >> kTileWLog);
           }
           if (px < P.W && lrow < P.rows) {
             py = (P.stripe_count == 1)
@@ -1823,7 +1836,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
       } else if (finish) {
         if (P.tile_cost) {   // cost of this sample: its bounces, or in time mode the pixel's lifetime at its
                              // last sample, summed per tile position over the launch's frames
-          const long long t = (long long)(lrow >> 3) * P.tiles_x + (px >> 3);   // tile position (all frames)
+          const long long t = (long long)(lrow >> kTileHLog) * P.tiles_x + (px >> kTileWLog);   // tile position (all frames)
           uint32_t c = (uint32_t)(depth + 1);
           if (P.cost_time) {
             c = 0;
@@ -2724,9 +2737,9 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   P.rows = rows;
   P.out_global = (p->flags & RT_FLAG_GLOBAL_ROWS) ? 1 : 0;
   if (P.out_global && list) return fail(RT_ERR_INVALID, "RT_FLAG_GLOBAL_ROWS is not supported by the adaptive pass");
-  P.tiles_x = (P.W + 7) / 8;
+  P.tiles_x = (P.W + kTileW - 1) / kTileW;
   P.nsamp = p->spp_n * p->spp_n;
-  P.frame_tiles = list ? (list_cap * P.nsamp + 63) / 64 : (long long)P.tiles_x * ((rows + 7) / 8);
+  P.frame_tiles = list ? (list_cap * P.nsamp + 63) / 64 : (long long)P.tiles_x * ((rows + kTileH - 1) / kTileH);
   P.n_tiles = P.frame_tiles * n_frames;
   if (P.n_tiles >= (1LL << 31)) return fail(RT_ERR_INVALID, "rt_launch: more than 2^31 tiles in one launch");
   P.div_row_tiles = div_magic((uint32_t)P.tiles_x * (uint32_t)n_frames);
@@ -2755,7 +2768,7 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   const bool cost_order = !list && n_frames == 1 && ((p->flags & RT_FLAG_COST_ORDER) || implicit_order);
   const bool cost_debug = !list && (p->flags & (RT_FLAG_TILE_COST | RT_FLAG_TILE_COST_TIME));
   if (cost_order || cost_debug) {
-    const long long n_pos = (long long)P.tiles_x * ((rows + 7) / 8);
+    const long long n_pos = (long long)P.tiles_x * ((rows + kTileH - 1) / kTileH);
     if (sc->cost_cap < n_pos) {
       HIP_TRY(hipDeviceSynchronize());   // launches in flight may still use the old buffers
       for (uint32_t*& q : sc->d_cost) { if (q) HIP_TRY(hipFree(q)); q = nullptr; }
@@ -3202,6 +3215,13 @@ long long rt_debug_wave_log(rt_scene* sc, unsigned long long* out, long long n) 
   HIP_TRY(hipMemcpy(out, sc->ctx[sc->last_ctx].d_wavelog, (size_t)words * sizeof(unsigned long long),
                     hipMemcpyDeviceToHost));
   return words;
+}
+
+int rt_tile_shape(int* tile_w, int* tile_h) {
+  if (!tile_w || !tile_h) return fail(RT_ERR_INVALID, "rt_tile_shape: null argument");
+  *tile_w = kTileW;
+  *tile_h = kTileH;
+  return RT_OK;
 }
 
 int rt_ipc_get_handle(const void* d_ptr, unsigned char* handle, unsigned long long* offset) {

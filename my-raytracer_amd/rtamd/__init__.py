@@ -409,6 +409,13 @@ class DeviceScene:
         return ms.value
 
 
+def tile_shape():
+    """(width, height) of the render kernel's work tile (rt_tile_shape)."""
+    w, h = C.c_int(0), C.c_int(0)
+    _check_hip(hip_lib().rt_tile_shape(C.byref(w), C.byref(h)), "rt_tile_shape")
+    return w.value, h.value
+
+
 def ipc_handle(d_ptr):
     """(handle bytes, offset) exporting the device allocation that holds d_ptr to other
     processes (rt_ipc_get_handle)."""

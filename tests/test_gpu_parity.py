@@ -271,14 +271,16 @@ def test_tile_order_and_costs_change_no_pixel(nf):
         return [o.cpu().numpy().copy() for o in outs], counts(st)
 
     ref, rc = render()
-    n_tiles = 25 * 15 * nf
+    tw, th = rtamd.tile_shape()
+    n_pos = -(-200 // tw) * -(-113 // th)   # tile positions of one frame
+    n_tiles = n_pos * nf
     for flag in (rtamd.abi.RT_FLAG_TILE_COST, rtamd.abi.RT_FLAG_TILE_COST_TIME, rtamd.abi.RT_FLAG_COST_ORDER,
                  rtamd.abi.RT_FLAG_COST_ORDER, rtamd.abi.RT_FLAG_COST_ORDER,
                  rtamd.abi.RT_FLAG_COST_ORDER):   # (one-frame: ordered from the third on, by the costs of two before)
         img, c = render(flag)
         assert all(np.array_equal(a, b) for a, b in zip(img, ref)) and c == rc
         n = lib.rt_debug_tile_cost(dev._h, None, 0)
-        assert n == 25 * 15   # tile positions (summed over the frames)
+        assert n == n_pos   # tile positions (summed over the frames)
         cost = np.zeros(n, dtype=np.uint32)
         lib.rt_debug_tile_cost(dev._h, cost.ctypes.data_as(C.POINTER(C.c_uint)), n)
         assert cost.min() > 0
@@ -287,7 +289,7 @@ def test_tile_order_and_costs_change_no_pixel(nf):
         # their costs too; RT_FLAG_NATURAL_ORDER records nothing and leaves the last map as it was)
         img, c = render(0)
         assert all(np.array_equal(a, b) for a, b in zip(img, ref)) and c == rc
-        cost = np.zeros(25 * 15, dtype=np.uint32)
+        cost = np.zeros(n_pos, dtype=np.uint32)
         lib.rt_debug_tile_cost(dev._h, cost.ctypes.data_as(C.POINTER(C.c_uint)), cost.size)
         assert cost.min() > 0
         img, c = render(rtamd.abi.RT_FLAG_NATURAL_ORDER)
