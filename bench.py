@@ -138,11 +138,13 @@ def parse():
     ap.add_argument("--reserve-ab", choices=["auto", "on", "off"], default="auto",
                     help="N > 1: after the timed run, time the same run again with the other reserve_cus setting "
                          "(32 if the run used 0, else 0) and report both (multi_gpu.reserve_cus_ab); auto = on at N > 1")
-    ap.add_argument("--assembly", choices=["gather", "peer"], default="gather",
+    ap.add_argument("--assembly", choices=["auto", "gather", "peer"], default="auto",
                     help="N > 1 frame assembly on rank 0: gather = one RCCL gather of every launch's stripes + "
-                         "re-interleave (default); peer = every rank's render writes its stripes straight into rank "
-                         "0's frame over xGMI (RT_FLAG_GLOBAL_ROWS, IPC-mapped buffers) and one RCCL all_reduce per "
-                         "launch fences it (rtamd.shard.PeerFrames)")
+                         "re-interleave; peer = every rank's render writes its stripes straight into rank 0's frame "
+                         "over xGMI (RT_FLAG_GLOBAL_ROWS, IPC-mapped buffers) and one RCCL all_reduce per launch "
+                         "fences it (rtamd.shard.PeerFrames); auto (default) = before the warm-up, two untimed "
+                         "launches in each, the faster one if both assembled bit-identical frames, else gather "
+                         "(multi_gpu.assembly_choice)")
     ap.add_argument("--assembly-ab", choices=["auto", "on", "off"], default="auto",
                     help="N > 1: after the timed run, time the same run with the other assembly and check that both "
                          "assemble bit-identical frames (multi_gpu.assembly_ab); auto = on at N > 1 without --adaptive")
@@ -360,7 +362,7 @@ def main():
     # the launches write global rows (RT_FLAG_GLOBAL_ROWS)
     if a.adaptive and a.assembly == "peer":
         raise SystemExit("bench.py: --assembly peer does not support --adaptive")
-    assembly = a.assembly if n > 1 else "gather"
+    assembly = a.assembly if n > 1 and not a.adaptive else "gather"
     peer = None
 
     def peer_frames():
@@ -480,6 +482,39 @@ def main():
         g_ms = float(np.mean([s_.elapsed_time(e_) for s_, e_ in zip(gstarts, gends)])) if gstarts else 0.0
         return el, k_ms, g_ms
 
+    def choose_assembly():
+        """--assembly auto (N > 1): both assemblies render the same two launches of F frames (after one
+        warm-up launch each, untimed for the result); peer wins if it was faster and its frames equal the
+        gather's bit for bit on rank 0.  A rank that cannot map rank 0's frames makes it gather."""
+        nonlocal assembly
+        err = ""
+        try:
+            peer_frames()
+        except Exception as e:   # IPC mapping refused on this rank
+            err = repr(e)
+        ok = torch.tensor([0.0 if err else 1.0], dtype=torch.float64, device="cuda")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if ok[0] < 1.0:
+            return "gather", {"chosen": "gather", "reason": "peer mapping failed" + (f" here: {err}" if err else
+                                                                                       " on another rank")}
+        secs, frames = {}, {}
+        for mode in ("gather", "peer"):
+            assembly = mode
+            run(F, False)
+            secs[mode] = timed_region(lambda: run(2 * F, False))
+            frames[mode] = image.clone() if rank == 0 else None
+        same = torch.tensor([float(torch.equal(frames["gather"], frames["peer"])) if rank == 0 else 0.0],
+                            dtype=torch.float64, device="cuda")
+        dist.broadcast(same, src=0)
+        identical = bool(same[0] == 1.0)
+        chosen = "peer" if identical and secs["peer"] < secs["gather"] else "gather"
+        return chosen, {"chosen": chosen, "frames_identical": identical,
+                        "calibration_ms_per_frame": {k: round(v / (2 * F) * 1e3, 4) for k, v in secs.items()},
+                        "rule": "two untimed launches of F frames in each assembly; peer if faster and bit-identical"}
+
+    assembly_choice = None
+    if assembly == "auto":
+        assembly, assembly_choice = choose_assembly()
     elapsed, kernel_ms_avg, gather_ms_avg = timed_run(a.warmup)
     frames_per_launch = float(np.mean(launch_frames))
     last_image = image
@@ -502,6 +537,7 @@ def main():
                  "gather_MB_per_launch_into_rank0": round((n - 1) * frames_per_launch * rows_max * W * 3 * 4 / 1e6, 2),
                  "reserve_cus": int(upload_opts.get("reserve_cus", 0)),
                  "assembly": assembly,
+                 "assembly_choice": assembly_choice,
                  "def": "render = HIP events around each launch on its stream; gather = HIP events around the "
                         "collective of its frames' stripes + rank 0's re-interleave (peer assembly: around the "
                         "fence all_reduce) -- includes waiting for the slowest rank's render; means over the "

@@ -395,9 +395,9 @@ int rt_debug_blocks_per_cu(rt_scene* scene, int variant);
  * words copied. */
 long long rt_debug_timeline(rt_scene* scene, unsigned long long* out, long long n);
 
-/* The render kernel's work tile: one wave's 64 pixels, *tile_w x *tile_h (16 x 4: a tile row of
- * fp32 RGB is 192 B, whole 64-B write units of the image).  Tile positions of the diagnostics
- * below are ty * ceil(width / tile_w) + tx over the shard's ceil(rows / tile_h) tile rows. */
+/* The render kernel's work tile: one wave's 64 pixels, *tile_w x *tile_h (8 x 8).  Tile positions
+ * of the diagnostics below are ty * ceil(width / tile_w) + tx over the shard's
+ * ceil(rows / tile_h) tile rows. */
 int rt_tile_shape(int* tile_w, int* tile_h);
 
 /* Diagnostics (tile-order experiments): the per-tile-position cost map of the last launch with

@@ -24,7 +24,7 @@
 //   * rays live in LDS slots (fp64 origin / direction / t-limit + 3 aux words
 //     holding the hit's barycentrics or the bounce normal); idle lanes are lent
 //     to owners for their extra shadow rays and reflection ray (fan-out);
-//   * work distribution: persistent workgroups pull 16x4 pixel tiles from 8
+//   * work distribution: persistent workgroups pull 8x8 pixel tiles from 8
 //     work heads on separate cache lines, one per XCD group, refilled per wave
 //     with a single atomic when >= kRefill lanes are idle; several frames per
 //     launch share the queue in band-major order (each head serves one row band
@@ -533,13 +533,13 @@ __device__ __forceinline__ TriOps load_tri(const GTri* tris, uint32_t i) {
   return T;
 }
 
-// Work tiles: one wave's 64 pixels, kTileW x kTileH.  16 x 4 (round 5): a tile row is 16 fp32
-// RGB pixels = 192 B, three whole 64-B write units of the image (rows of 1920 px are 64-B aligned),
-// where 8 x 8 tiles (round 1-4) wrote 96-B row segments that straddle them: HBM writes of the image
-// were 36.2 MB per office frame for 24.9 MB of pixels (profiles/r05/r05e_write_attrib_*); the
-// unit is also the grain of the cost order (rt_debug_tile_cost and friends).
+// Work tiles: one wave's 64 pixels, kTileW x kTileH, 8 x 8 (the most coherent primary rays); the
+// unit is also the grain of the cost order (rt_debug_tile_cost and friends).  A tile row of fp32
+// RGB is a 96-B segment, which straddles the image's 64-B HBM write units: the office's 24.9 MB
+// image costs 36.2 MB of HBM writes per frame.  16 x 4 tiles (192-B segments, whole units) cut that
+// to 28.9 MB but cost 2.9 % batched / 3.9 % one frame, 32 x 2 cost 9 % (profiles/r05/r05g_*).
 #ifndef RT_TILE_W
-#define RT_TILE_W 16
+#define RT_TILE_W 8
 #endif
 constexpr int kTileW = RT_TILE_W, kTileH = 64 / RT_TILE_W;
 constexpr int kTileWLog = kTileW == 8 ? 3 : kTileW == 16 ? 4 : kTileW == 32 ? 5 : -1;

@@ -85,9 +85,16 @@ class PeerFrames:
         self.elem = torch.empty((), dtype=dtype).element_size()
         self.images = [torch.zeros(lead + (height, width, channels), dtype=dtype, device=device)
                        for _ in range(slots)] if rank == 0 else None
-        handles = [[ipc_handle(im.data_ptr()) for im in self.images]] if rank == 0 else [None]
+        handles = [None]
+        if rank == 0:
+            try:
+                handles = [[ipc_handle(im.data_ptr()) for im in self.images]]
+            except Exception as e:   # every rank learns of it (no rank left waiting in the broadcast)
+                handles = [f"rank 0: {e!r}"]
         if n > 1:
             dist.broadcast_object_list(handles, src=0)
+        if isinstance(handles[0], str):
+            raise RuntimeError(f"PeerFrames: exporting the frame buffers failed ({handles[0]})")
         dev = torch.device(device).index if torch.device(device).index is not None else torch.cuda.current_device()
         self._opened = []
         if rank == 0:

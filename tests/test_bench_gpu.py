@@ -139,7 +139,7 @@ def test_bench_peer_assembly_two_ranks(tmp_path):
     d = json.loads(r.stdout.strip().splitlines()[-1])
     m = d["multi_gpu"]
     assert d["n_gpus"] == 2 and m["assembly"] == "peer" and m["assembly_ab"]["frames_identical"] is True
-    assert "reserve_cus_ab" not in m
+    assert "reserve_cus_ab" not in m and m["assembly_choice"] is None   # given, not chosen
     ref, rays = expected_frames(320, 180, 8)
     assert np.array_equal(np.load(out), ref)
     assert d["config"]["rays_per_frame"] == rays
@@ -176,10 +176,14 @@ def test_bench_four_ranks_driver_shape(tmp_path):
     assert set(ab) == {"0", "32"} and ab["0"]["value"] == d["value"]
     for rec in ab.values():
         assert rec["value"] > 0 and rec["render_ms_per_launch_max"] > 0 and rec["gather_ms_per_launch_rank0"] > 0
-    # the other frame assembly (peer stores into rank 0's frame + a fence), bit-identical frames
-    assert m["assembly"] == "gather"
+    # assembly auto: both assemblies calibrated on the same launches, bit-identical frames; the other
+    # one timed as well (assembly_ab), its frames bit-identical too
+    ch = m["assembly_choice"]
+    assert ch["frames_identical"] is True and ch["chosen"] == m["assembly"] in ("gather", "peer")
+    assert set(ch["calibration_ms_per_frame"]) == {"gather", "peer"}
     asm = m["assembly_ab"]
-    assert asm["frames_identical"] is True and asm["gather"]["value"] == d["value"] and asm["peer"]["value"] > 0
+    other = "peer" if m["assembly"] == "gather" else "gather"
+    assert asm["frames_identical"] is True and asm[m["assembly"]]["value"] == d["value"] and asm[other]["value"] > 0
     ref, rays = expected_frames(320, 180, 10)
     assert np.array_equal(np.load(out), ref)
     assert d["config"]["rays_per_frame"] == rays
