@@ -386,49 +386,6 @@ __device__ __forceinline__ double det3(D3 v1, D3 v2, D3 v3) {
          v3.x * (v1.y * v2.z - v2.y * v1.z);
 }
 
-#ifdef RT_TRI_F32
-// fp32 pre-test of the triangle test (A/B variant RT_TRI_F32): the CPU's S, Da, Db recomputed in
-// fp32 from the rounded fp64 operands, each with a bound on its error.  For a 3x3 determinant of
-// three columns rounded to fp32 (relative 2^-24 each) and evaluated as a.(b x c) with fma, the
-// error is at most ~8 u P, u = 2^-24, P = |a|.(|b| x |c|) (the permanent of the absolute values;
-// the fp64 reference's own error, ~8 x 2^-53 P, is far below): 2^-19 P bounds both with a factor 2
-// to spare, plus 2^-100 absolute for flushed denormals.  rejects() is true only where the fp64
-// test certainly rejects: sign(S) is certain, and alpha < 0 or beta < 0 (the numerator's sign is
-// certain, and |numerator| > 2^-64 |S| so the fp64 quotient is no -0) or gamma < 0 (its fp32 value
-// below minus its bound, which exceeds the fp64 gamma's error 2^-51 (1 + |alpha| + |beta|)).
-// NaN or inf anywhere makes every comparison false: no rejection.
-struct F3 { float x, y, z; };
-__device__ __forceinline__ F3 f3_of(D3 v) { return F3{(float)v.x, (float)v.y, (float)v.z}; }
-__device__ __forceinline__ F3 cross_f(F3 a, F3 b) {
-  return F3{__builtin_fmaf(a.y, b.z, -(a.z * b.y)), __builtin_fmaf(a.z, b.x, -(a.x * b.z)),
-            __builtin_fmaf(a.x, b.y, -(a.y * b.x))};
-}
-__device__ __forceinline__ F3 cross_abs(F3 a, F3 b) {   // |a| x |b| with + (the permanent's terms)
-  return F3{__builtin_fmaf(fabsf(a.y), fabsf(b.z), fabsf(a.z) * fabsf(b.y)),
-            __builtin_fmaf(fabsf(a.z), fabsf(b.x), fabsf(a.x) * fabsf(b.z)),
-            __builtin_fmaf(fabsf(a.x), fabsf(b.y), fabsf(a.y) * fabsf(b.x))};
-}
-__device__ __forceinline__ float dot_f(F3 a, F3 b) { return __builtin_fmaf(a.z, b.z, __builtin_fmaf(a.y, b.y, a.x * b.x)); }
-__device__ __forceinline__ float dot_abs(F3 a, F3 b) {
-  return __builtin_fmaf(fabsf(a.z), b.z, __builtin_fmaf(fabsf(a.y), b.y, fabsf(a.x) * b.x));
-}
-__device__ __forceinline__ bool tri_f32_rejects(D3 e1d, D3 e2d, D3 c4d, D3 c3d) {
-  const F3 e1 = f3_of(e1d), e2 = f3_of(e2d), c4 = f3_of(c4d), c3 = f3_of(c3d);
-  const F3 X = cross_f(e2, c3), Y = cross_f(e1, c3);
-  const F3 AX = cross_abs(e2, c3), AY = cross_abs(e1, c3);
-  const float S = dot_f(e1, X), Da = dot_f(c4, X), Db = -dot_f(c4, Y);
-  const float eS = __builtin_fmaf(dot_abs(e1, AX), 0x1p-19f, 0x1p-100f);
-  const float eA = __builtin_fmaf(dot_abs(c4, AX), 0x1p-19f, 0x1p-100f);
-  const float eB = __builtin_fmaf(dot_abs(c4, AY), 0x1p-19f, 0x1p-100f);
-  if (!(fabsf(S) > eS)) return false;   // sign of S uncertain (or NaN)
-  const float sg = S > 0.0f ? 1.0f : -1.0f;
-  const float ua = Da * sg, ub = Db * sg, aS = fabsf(S);
-  const bool a_neg = ua < -2.0f * eA && fabsf(Da) * 0x1p64f >= aS;
-  const bool b_neg = ub < -2.0f * eB && fabsf(Db) * 0x1p64f >= aS;
-  const bool g_neg = (aS - ua - ub) < -2.0f * (eS + eA + eB);
-  return a_neg || b_neg || g_neg;
-}
-#endif
 
 // Analytic hits in fp64, the oracle's operation order (oracle/rt_oracle.c plane_hit /
 // sphere_hit, myplane.cpp:22-49); returns the hit distance or DBL_MAX.
@@ -1094,9 +1051,6 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
       uint32_t sq = 0, sqlim = kRingB;
       bool susp_now = false;   // SUSP: this lane's traversal is parked at the end of this phase
       uint32_t susp_pleaf = kDone;
-#ifdef RT_PLEAF2
-      uint32_t susp_pleaf2 = kDone;
-#endif
       if constexpr (SUSP) {
         // the parked record: {cur | postponed leaf << 32, sp | slo << 16 | shadow hit << 31 | best << 32,
         // best slot, t-limit}; the ray setup above is recomputed bit for bit from the slot
@@ -1112,9 +1066,6 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
           shadow_hit = ((w1 >> 31) & 1ull) != 0ull;
           best = (int)(uint32_t)(w1 >> 32);
           best_slot = (int)(uint32_t)__double_as_longlong(b.a);
-#ifdef RT_PLEAF2
-          susp_pleaf2 = (uint32_t)((unsigned long long)__double_as_longlong(b.a) >> 32);
-#endif
           tlim = b.b;
           hi_c = round_up_f(tlim - t_off);
         }
@@ -1180,10 +1131,6 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
             // rejections first: they fire only where the CPU's rounded quotients certainly
             // fail the same test (margins in DESIGN.md §4), so accept decisions are unchanged.
             const D3 c4 = sub(ro, T.p2);
-#ifdef RT_TRI_F32
-            if (!tri_f32_rejects(T.e1, T.e2, c4, c3))
-#endif
-            {
             const double S = det3(T.e1, T.e2, c3);
             if (fabs(S) >= 1e-10) {
               const double Da = det3(c4, T.e2, c3);
@@ -1196,14 +1143,6 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
                                (Da + Db - S) * sS > 0x1p-40 * (fabs(Da) + fabs(Db) + aS);
               if (!out) {
                 const double Dt = det3(T.e1, T.e2, c4);
-#ifdef RT_TRI_TREJ
-                // A/B variant: t = Dt / S only where it can pass.  With uD = Dt sgn(S), t = uD / |S|
-                // exactly; uD <= fl(1e-5 |S|)(1 - 2^-40) proves t <= 1e-5, and uD >= fl(tlim |S|)
-                // (1 + 2^-39) proves t >= tlim (1 + 2^-40) > tlim after rounding (reject either way)
-                const double uD = Dt * sS;
-                if (!(uD <= (1e-5 * aS) * (1.0 - 0x1p-40)) && !(uD >= (tlim * aS) * (1.0 + 0x1p-39)))
-#endif
-                {
                 // (t's division shared with alpha / beta's reciprocal: -0.9 %, more live registers)
                 const double t = Dt / S;
                 const bool cand = anyhit ? (t < tlim) : (t <= tlim);
@@ -1244,9 +1183,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
                     }
                   }
                 }
-                }
               }
-            }
             }
             if (T.meta & (WIDTH == 2 ? kLastRef : kLastDev)) break;
             ++i;
@@ -1255,16 +1192,8 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
           return occluded;
       };
       uint32_t pleaf = kDone;   // 4-wide: postponed leaf
-#ifdef RT_PLEAF2
-      // A/B variant: up to two postponed leaves per lane before the wave votes for the leaf phase
-      // (more leaf work per leaf-phase iteration; t-culling and occlusion found later)
-      uint32_t pleaf2 = kDone;
-#endif
       if constexpr (SUSP) {
         if (resumed) pleaf = susp_pleaf;
-#ifdef RT_PLEAF2
-        if (resumed) pleaf2 = susp_pleaf2;
-#endif
       }
 
       uint32_t rounds = 0;
@@ -1292,14 +1221,8 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
                                             ((unsigned long long)(uint32_t)best << 32);
               buf_st(prs, pvo, (uint32_t)R_SUSP * kRegionBytes, __longlong_as_double((long long)w0));
               buf_st(prs, pvo, (uint32_t)R_SUSP * kRegionBytes + 8u, __longlong_as_double((long long)w1));
-#ifdef RT_PLEAF2
-              buf_st(prs, pvo, (uint32_t)R_SUSP * kRegionBytes + 16u,
-                     __longlong_as_double((long long)((unsigned long long)(uint32_t)best_slot |
-                                                      ((unsigned long long)pleaf2 << 32))));
-#else
               buf_st(prs, pvo, (uint32_t)R_SUSP * kRegionBytes + 16u,
                      __longlong_as_double((long long)(unsigned long long)(uint32_t)best_slot));
-#endif
               buf_st(prs, pvo, (uint32_t)R_SUSP * kRegionBytes + 24u, tlim);
               susp_now = true;
             }
@@ -1429,24 +1352,11 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
           }
           }
 #undef RT_CSWAP
-#ifdef RT_PLEAF2
-          if ((cur & kLeaf) && cur != kDone) {   // first / second leaf: postpone, keep going
-            if (pleaf == kDone) {
-              pleaf = cur;
-              cur = pop();
-            } else if (pleaf2 == kDone) {
-              pleaf2 = cur;
-              cur = pop();
-            }
-          }
-          if ((wballot(pleaf2 == kDone) & wballot(cur != kDone)) == 0) break;   // every lane holds two leaves or is done
-#else
           if ((cur & kLeaf) && cur != kDone && pleaf == kDone) {   // first leaf: postpone, keep going
             pleaf = cur;
             cur = pop();
           }
           if ((wballot(pleaf == kDone) & wballot(cur != kDone)) == 0) break;   // every lane holds a leaf (one mask per compare)
-#endif
         }
         }
         // leaves: 2-wide -- the leaf the lane stopped at; 4-wide -- the postponed leaf, then
@@ -1466,19 +1376,10 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
             if (test_leaf(pleaf)) {   // any-hit: occluded, the ray is finished
               cur = kDone;
               pleaf = kDone;
-#ifdef RT_PLEAF2
-              pleaf2 = kDone;
-#endif
               break;
             }
-#ifdef RT_PLEAF2
-            pleaf = pleaf2;
-            pleaf2 = kDone;
-            if (pleaf == kDone && (cur & kLeaf) && cur != kDone) {
-#else
             pleaf = kDone;
             if ((cur & kLeaf) && cur != kDone) {
-#endif
               pleaf = cur;
               cur = pop();
             }
