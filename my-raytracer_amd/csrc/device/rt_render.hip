@@ -517,8 +517,7 @@ static_assert(kTileWLog > 0 && kTileW * kTileH == 64, "a tile is one wave's 64 p
 //     fit one batch restarts from the recomputed ambient term).
 // The mirror coefficient comes from the material (the lane keeps the mesh id); the normal of
 // the bounce being shaded lives in the slot's aux words (below).
-//   a suspended traversal (R_SUSP, SUSP variants: cur, postponed leaf, stack pointers, hit so far).
-enum : int { R_SCOLW = 0, R_PCOL = 1, R_HD = 2, R_LACC = 3, R_SUSP = 4, kRegions = 5 };
+enum : int { R_SCOLW = 0, R_PCOL = 1, R_HD = 2, R_LACC = 3, kRegions = 4 };
 constexpr uint32_t kLaneRec = 32;                 // bytes per lane and region
 constexpr uint32_t kRegionBytes = 64 * kLaneRec;  // 2 KB per wave and region
 
@@ -609,14 +608,7 @@ __device__ void order_range(const uint32_t* cost, uint32_t* order, long long n_t
   }
 }
 
-// SUSP: suspend/resume traversal -- once at most kSuspActive lanes of a wave still traverse and work
-// is left, the wave leaves the traversal with those lanes' traversal state parked in path state
-// (R_SUSP; their stacks stay in the LDS ring / spill area), shades its finished lanes, refills its
-// idle ones and resumes the parked rays beside the new ones.  Raises SIMD efficiency where rays of a
-// wave differ widely in length (incoherent scenes); no fan-out in these variants.
-constexpr int kSuspBit = 8;
-constexpr int kSuspActive = 16;   // 16 (config 4: 8 +2.8 %, 16 +3.2 %, 32 +1.8 %, 48 -8 %)
-template <int WIDTH, bool STATS, bool TL = false, int RING = kShortStack, bool SUSP = false>
+template <int WIDTH, bool STATS, bool TL = false, int RING = kShortStack>
 __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_kernel(KParams P) {
   static_assert(RING >= kMigWords && (RING & (RING - 1)) == 0, "ring: a power of two holding the migration words");
   constexpr int kRingMask = RING - 1;
@@ -692,7 +684,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
   };
   auto ST4 = [&](int r, D3 v, double w) {
 #ifdef RT_MEAS_NO_PSTATE   // write-attribution build (wrong colours, same control flow): no path-state stores
-    if (r != R_SUSP) return;
+    return;
 #endif
     const uint32_t o = (uint32_t)r * kRegionBytes;
     buf_st(prs, pvo, o, v.x); buf_st(prs, pvo, o + 8u, v.y); buf_st(prs, pvo, o + 16u, v.z); buf_st(prs, pvo, o + 24u, w);
@@ -930,11 +922,6 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
     }
     // ================= TRAVERSE phase =================
     {
-      bool resumed = false;   // SUSP: this lane's ray resumes a parked traversal
-      if constexpr (SUSP) {
-        resumed = (state & kSuspBit) != 0;
-        state &= ~kSuspBit;
-      }
       const bool anyhit = (state == ST_SHADOW || state == ST_HSHADOW);
       // helpers read their owner's slot (its closest-hit ray and hit distance)
       const int src = (state >= ST_HSHADOW) ? wbase + (int)(htask & 63u) : (int)threadIdx.x;
@@ -1049,27 +1036,6 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
       // below kSW) and one add; sp / slo themselves are only formed on the spill path
       constexpr uint32_t kSW = kBlock * 4u, kRingB = (uint32_t)RING * kSW, kRingBMask = (uint32_t)kRingMask * kSW;
       uint32_t sq = 0, sqlim = kRingB;
-      bool susp_now = false;   // SUSP: this lane's traversal is parked at the end of this phase
-      uint32_t susp_pleaf = kDone;
-      if constexpr (SUSP) {
-        // the parked record: {cur | postponed leaf << 32, sp | slo << 16 | shadow hit << 31 | best << 32,
-        // best slot, t-limit}; the ray setup above is recomputed bit for bit from the slot
-        if (resumed) {
-          const D2 a = buf_ld2(prs, pvo, (uint32_t)R_SUSP * kRegionBytes);
-          const D2 b = buf_ld2(prs, pvo, (uint32_t)R_SUSP * kRegionBytes + 16u);
-          const unsigned long long w0 = (unsigned long long)__double_as_longlong(a.a);
-          const unsigned long long w1 = (unsigned long long)__double_as_longlong(a.b);
-          cur = (uint32_t)w0;
-          susp_pleaf = (uint32_t)(w0 >> 32);
-          sq = (uint32_t)(w1 & 0xffffu) * kSW;
-          sqlim = ((uint32_t)((w1 >> 16) & 0x7fffu) + (uint32_t)RING) * kSW;
-          shadow_hit = ((w1 >> 31) & 1ull) != 0ull;
-          best = (int)(uint32_t)(w1 >> 32);
-          best_slot = (int)(uint32_t)__double_as_longlong(b.a);
-          tlim = b.b;
-          hi_c = round_up_f(tlim - t_off);
-        }
-      }
       auto ring = [&](uint32_t q) -> __attribute__((address_space(3))) uint32_t& {
         return *reinterpret_cast<__attribute__((address_space(3))) uint32_t*>((size_t)((q & kRingBMask) | lane_b));
       };
@@ -1192,9 +1158,6 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
           return occluded;
       };
       uint32_t pleaf = kDone;   // 4-wide: postponed leaf
-      if constexpr (SUSP) {
-        if (resumed) pleaf = susp_pleaf;
-      }
 
       uint32_t rounds = 0;
       // a wave whose traversing lanes are all any-hit rays visits children without the distance
@@ -1210,24 +1173,6 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
           cur = kDone;
           pleaf = kDone;
           break;
-        }
-        if constexpr (SUSP) {
-          // few lanes left and work to fetch: park the rest, shade and refill, resume next phase
-          if (heads_left > 0 && __popcll(wballot(cur != kDone) | wballot(pleaf != kDone)) <= kSuspActive) {
-            if (cur != kDone || pleaf != kDone) {
-              const unsigned long long w0 = (unsigned long long)cur | ((unsigned long long)pleaf << 32);
-              const unsigned long long w1 = (unsigned long long)((sq / kSW) | (((sqlim - kRingB) / kSW) << 16) |
-                                                                  (shadow_hit ? 0x80000000u : 0u)) |
-                                            ((unsigned long long)(uint32_t)best << 32);
-              buf_st(prs, pvo, (uint32_t)R_SUSP * kRegionBytes, __longlong_as_double((long long)w0));
-              buf_st(prs, pvo, (uint32_t)R_SUSP * kRegionBytes + 8u, __longlong_as_double((long long)w1));
-              buf_st(prs, pvo, (uint32_t)R_SUSP * kRegionBytes + 16u,
-                     __longlong_as_double((long long)(unsigned long long)(uint32_t)best_slot));
-              buf_st(prs, pvo, (uint32_t)R_SUSP * kRegionBytes + 24u, tlim);
-              susp_now = true;
-            }
-            break;
-          }
         }
         if (STATS) wave_tick(d_round_it, d_round_ln, lane);
         if constexpr (TL) wave_tick(tl_wr, tl_dummy, lane);
@@ -1387,9 +1332,6 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
         }
       }
       thit = tlim;
-      if constexpr (SUSP) {
-        if (susp_now) state |= kSuspBit;
-      }
     }
     asm volatile("" ::: "memory");
     if (STATS) { const unsigned long long t = stamp(); d_trav += t - t_stamp; t_stamp = t; }
@@ -1451,9 +1393,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
       const int wib = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
       const bool owner = (state == ST_CLOSEST || state == ST_SHADOW);
       const unsigned long long O = wballot(owner);
-      // (a wave with parked traversals keeps them: their stacks live in its LDS ring entries)
-      if (O != 0ull && __popcll(O) <= kDonateMax && *pool_live >= 2u &&
-          (!SUSP || wballot((state & kSuspBit) != 0) == 0ull)) {
+      if (O != 0ull && __popcll(O) <= kDonateMax && *pool_live >= 2u) {
         // registers -> this thread's LDS stack entries, then publish the lane mask
         if (owner) {
           // packed: state (3 bits) | shadow hit | frame (< 128) | sample (< 4096) | refl_h + 1 (9 bits);
@@ -1580,7 +1520,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
         refl_h = -1;
         // extra lights of this batch, then the reflection ray once the batch covers every light
         const int rest = P.n_lights - light - 1;
-        want = SUSP ? 0 : min(rest, kBatchExtra) + ((rest <= kBatchExtra && mirror_ > 0.0 && depth < P.max_depth) ? 1 : 0);
+        want = min(rest, kBatchExtra) + ((rest <= kBatchExtra && mirror_ > 0.0 && depth < P.max_depth) ? 1 : 0);
       };
       if (state == ST_SHADOW) {   // batch finished: lights [light, batch_end) in order
         {   // the hit again, from the closest-hit ray and distance kept in the slot
@@ -2092,19 +2032,19 @@ struct Variant {
 // [0] production (4-wide), [1] 4-wide + counters, [2] canonical 2-wide counters
 // (the traversal the oracle replicates: tests pin its node / triangle counts),
 // [3] production + per-round timeline (RT_FLAG_TIMELINE, diagnostics), [4] production with a
-// 16-entry stack ring (deep hierarchies), [5] the same with suspend/resume traversal (deep
-// hierarchies' several-frame launches).
+// 16-entry stack ring (deep hierarchies).  (A suspend/resume variant for deep scenes' several-frame
+// launches, rounds 3-4, was removed in round 5: +0.2 % on config 4 against 21-30 MB per frame of
+// parked-state writes)
 const Variant kVariants[] = {
     {render_kernel<4, false>, false},
     {render_kernel<4, true>, true},
     {render_kernel<2, true>, true},
     {render_kernel<4, false, true>, false},
     {render_kernel<4, false, false, 16>, false},
-    {render_kernel<4, false, false, 16, true>, false},
 };
-constexpr int kNumVariants = 6;
+constexpr int kNumVariants = 5;
 constexpr int kRingDeep = 16;
-inline int variant_ring(int v) { return (v == 4 || v == 5) ? kRingDeep : kShortStack; }
+inline int variant_ring(int v) { return v == 4 ? kRingDeep : kShortStack; }
 // LDS per block: the variant's stack ring (ring entries per thread, at address 0: the kernel's
 // slot offsets are compile-time constants), kSlotDoubles doubles of slot, task + visibility words.
 size_t lds_bytes(int /*stack_words*/, int ring = kShortStack) {
@@ -2726,13 +2666,7 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   const int v = (p->flags & RT_FLAG_TRAVERSAL_STATS) ? 2
                 : (p->flags & RT_FLAG_WIDE_STATS) ? 1
                 : (p->flags & RT_FLAG_TIMELINE) ? 3
-                // 4/5: the 16-entry-ring production variants; suspend/resume on deep scenes' several-
-                // frame launches (config 4, 128 frames: +3.2 %; one frame: -6 %, so not there)
-#ifdef RT_MEAS_NO_SUSP   // write-attribution build: deep scenes never suspend
-                : sc->deep ? 4
-#else
-                : sc->deep ? ((n_frames > 1 && !list) ? 5 : 4)
-#endif
+                : sc->deep ? 4   // the 16-entry-ring production variant
                 : 0;
   const int ring = variant_ring(v);
   const int n_top = sc->n_top_v[v];

@@ -908,10 +908,9 @@ def test_stack_ring_depth_changes_no_pixel(kind, kw, w, h, spp):
 
 
 @pytest.mark.parametrize("kw,w,h", [({"n_triangles": 200000}, 160, 90), ({"n_triangles": 300000}, 192, 108)])
-def test_suspend_resume_frames_equal_single_launches(kw, w, h):
-    # Deep scenes' several-frame launches run the suspend/resume variant (waves park their last
-    # few rays, shade and refill, then resume them): every frame equals its own one-frame launch
-    # (the plain deep variant) bit for bit, with the same ray counts, and the oracle.
+def test_deep_frames_equal_single_launches(kw, w, h):
+    # Deep scenes (the 16-entry-ring variant): every frame of a several-frame launch equals its own
+    # one-frame launch bit for bit, with the same ray counts, and the oracle.
     import torch
     hs, dev, orc = Case.get("random_tris", **kw)
     base = hs.render_params(w, h, 1)
