@@ -349,12 +349,14 @@ int rt_render_to_host(rt_scene* scene, const rt_render_params* p, void* host_out
  * RT_FLAG_GLOBAL_ROWS: every rank writes its stripes straight into rank 0's frame buffer).
  * rt_ipc_get_handle exports the device allocation that holds d_ptr (an RT_IPC_HANDLE_BYTES-byte
  * handle, plain bytes to send to the other processes) and d_ptr's byte offset in it.  Another
- * process maps it with rt_ipc_open, with its own `device` current (peer access over xGMI enabled
- * as needed), and gets a pointer to the same bytes; rt_ipc_close(ptr, offset) unmaps it.  The
+ * process maps it with rt_ipc_open, with its own `device` current and the exporter's device id as
+ * this process numbers it (`owner_device`, -1 = unknown: then the mapping's lazy peer access only):
+ * peer access from `device` to `owner_device` is checked and enabled, and the call returns a pointer
+ * to the same bytes; rt_ipc_close(ptr, offset) unmaps it.  The
  * exporting process must keep the allocation alive while it is mapped elsewhere. */
 #define RT_IPC_HANDLE_BYTES 64
 int rt_ipc_get_handle(const void* d_ptr, unsigned char* handle, unsigned long long* offset);
-int rt_ipc_open(const unsigned char* handle, unsigned long long offset, int device, void** d_ptr);
+int rt_ipc_open(const unsigned char* handle, unsigned long long offset, int device, int owner_device, void** d_ptr);
 int rt_ipc_close(void* d_ptr, unsigned long long offset);
 
 /* Milliseconds of the last launch on this scene, measured with hipEvents

@@ -3072,12 +3072,21 @@ int rt_ipc_get_handle(const void* d_ptr, unsigned char* handle, unsigned long lo
   return RT_OK;
 }
 
-int rt_ipc_open(const unsigned char* handle, unsigned long long offset, int device, void** d_ptr) {
+int rt_ipc_open(const unsigned char* handle, unsigned long long offset, int device, int owner_device, void** d_ptr) {
   if (!handle || !d_ptr) return fail(RT_ERR_INVALID, "rt_ipc_open: null argument");
   *d_ptr = nullptr;
   hipIpcMemHandle_t h;
   std::memcpy(&h, handle, sizeof h);
   HIP_TRY(hipSetDevice(device));
+  if (owner_device >= 0 && owner_device != device) {   // kernels on `device` will access the owner's memory
+    int can = 0;
+    HIP_TRY(hipDeviceCanAccessPeer(&can, device, owner_device));
+    if (!can) return fail(RT_ERR_UNSUPPORTED, "rt_ipc_open: the device cannot access the owner device's memory");
+    const hipError_t e = hipDeviceEnablePeerAccess(owner_device, 0);
+    if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+      return fail(RT_ERR_HIP, std::string("hipDeviceEnablePeerAccess: ") + hipGetErrorString(e));
+    (void)hipGetLastError();   // clear an already-enabled status
+  }
   void* base = nullptr;
   HIP_TRY(hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess));
   *d_ptr = reinterpret_cast<char*>(base) + offset;

@@ -425,13 +425,15 @@ def ipc_handle(d_ptr):
     return h.raw, off.value
 
 
-def ipc_open(handle, offset, device):
+def ipc_open(handle, offset, device, owner_device=-1):
     """Device pointer in this process (device `device` current) to the bytes another process
-    exported with ipc_handle (rt_ipc_open)."""
+    exported with ipc_handle from its device `owner_device` (this process's numbering; -1 =
+    unknown), with peer access from device to owner enabled (rt_ipc_open)."""
     if len(handle) != abi.RT_IPC_HANDLE_BYTES:
         raise ValueError("IPC handle must be RT_IPC_HANDLE_BYTES bytes")
     p = C.c_void_p(0)
-    _check_hip(hip_lib().rt_ipc_open(handle, C.c_ulonglong(offset), int(device), C.byref(p)), "rt_ipc_open")
+    _check_hip(hip_lib().rt_ipc_open(handle, C.c_ulonglong(offset), int(device), int(owner_device), C.byref(p)),
+               "rt_ipc_open")
     return int(p.value)
 
 

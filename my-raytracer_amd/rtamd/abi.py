@@ -181,7 +181,7 @@ HIP_SYMBOLS = {
     "rt_last_kernel_ms": (C.c_int, [C.c_void_p, C.POINTER(C.c_float)]),
     "rt_tile_shape": (C.c_int, [C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "rt_ipc_get_handle": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(C.c_ulonglong)]),
-    "rt_ipc_open": (C.c_int, [C.c_char_p, C.c_ulonglong, C.c_int, C.POINTER(C.c_void_p)]),
+    "rt_ipc_open": (C.c_int, [C.c_char_p, C.c_ulonglong, C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
     "rt_ipc_close": (C.c_int, [C.c_void_p, C.c_ulonglong]),
     "rt_debug_counters": (C.c_int, [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]),
     "rt_debug_wave_log": (C.c_longlong, [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_longlong]),

@@ -85,24 +85,25 @@ class PeerFrames:
         self.elem = torch.empty((), dtype=dtype).element_size()
         self.images = [torch.zeros(lead + (height, width, channels), dtype=dtype, device=device)
                        for _ in range(slots)] if rank == 0 else None
+        dev = torch.device(device).index if torch.device(device).index is not None else torch.cuda.current_device()
         handles = [None]
         if rank == 0:
-            try:
-                handles = [[ipc_handle(im.data_ptr()) for im in self.images]]
+            try:   # the handles, and rank 0's device (every rank sees the node's GPUs with the same ids)
+                handles = [([ipc_handle(im.data_ptr()) for im in self.images], dev)]
             except Exception as e:   # every rank learns of it (no rank left waiting in the broadcast)
                 handles = [f"rank 0: {e!r}"]
         if n > 1:
             dist.broadcast_object_list(handles, src=0)
         if isinstance(handles[0], str):
             raise RuntimeError(f"PeerFrames: exporting the frame buffers failed ({handles[0]})")
-        dev = torch.device(device).index if torch.device(device).index is not None else torch.cuda.current_device()
         self._opened = []
         if rank == 0:
             self.base = [im.data_ptr() for im in self.images]
         else:
             self.base = []
-            for h, off in handles[0]:
-                ptr = ipc_open(h, off, dev)
+            exported, owner = handles[0]
+            for h, off in exported:
+                ptr = ipc_open(h, off, dev, owner)
                 self._opened.append((ptr, off))
                 self.base.append(ptr)
         self.flag = torch.zeros(1, dtype=torch.float32, device=device)
