@@ -3,7 +3,7 @@
 # production render kernel, tools/pmc_summary.py with the committed calibration) of bench.py for
 # kernel libraries that each drop one writer (measurement builds, make variant V=-DRT_MEAS_*):
 #   RT_MEAS_NO_IMAGE   no image stores            RT_MEAS_NO_PSTATE  no path-state stores (colours only)
-#   RT_MEAS_NO_SUSP    deep scenes never suspend (parked traversal state)
+#   (round 5 also had RT_MEAS_NO_SUSP, for the suspend/resume variant removed since)
 # usage: tools/write_attrib.sh TAG "bench args" lib1.so[#opt=v,...] lib2.so ...
 set -e -o pipefail
 TAG=${1:?tag}; ARGS=$2; shift 2
