@@ -272,10 +272,14 @@ def main():
     F = 1 if (a.adaptive and not batched_adaptive) else max(1, min(a.frames or default_frames(a), rtamd.abi.RT_MAX_FRAMES,
                                                                    a.steps,
                                                                    int(a.frame_budget_gb * 1e9 // frame_bytes)))
-    if n > 1 and not a.frames and not a.adaptive:
-        # N > 1: at least two launches in the timed run, so the gather of one launch overlaps the
-        # rendering of the next (a single launch would leave its whole gather exposed)
-        F = min(F, max(1, (a.steps + 1) // 2))
+
+    def per_launch_of(mode):
+        """Frames per launch of the timed run.  N > 1 with the RCCL gather: at most half the steps,
+        so the run has two launches and the gather of one can overlap the next launch; the peer
+        assembly has nothing to overlap, so its frames go in launches of F (one drain per F)."""
+        if n > 1 and mode == "gather" and not a.frames and not a.adaptive:
+            return min(F, max(1, (a.steps + 1) // 2))
+        return F
     # the animation path: frame f of every launch (the batched frames are distinct views)
     if F > 1 and a.sweep != 0.0:
         cams = [rtamd.camera_orbit(params, a.sweep * (f / (F - 1) - 0.5)) for f in range(F)]
@@ -330,7 +334,16 @@ def main():
 
     n_full, rem = divmod(a.steps, F)
     st = launch_counts(F)
-    rays_timed_local = n_full * rays_of(st) + (rays_of(launch_counts(rem)) if rem else 0)
+    rays_cache = {}
+
+    def rays_timed_for(pl):
+        """This rank's rays in a.steps frames rendered pl at a time (launches of frames cams[:pl])
+        -- from untimed counting launches of exactly those shapes."""
+        if pl not in rays_cache:
+            nf_, rm_ = divmod(a.steps, pl)
+            rays_cache[pl] = nf_ * rays_of(launch_counts(pl)) + (rays_of(launch_counts(rm_)) if rm_ else 0)
+        return rays_cache[pl]
+    rays_adaptive_local = 0
     # the single-frame records render frames cams[0 .. NS) one per launch (an animation: distinct views)
     NS = max(1, min(a.single_frames, F))
     rays_frame0_local = rays_of(launch_counts(NS)) / NS  # rays per frame of those frames
@@ -339,15 +352,15 @@ def main():
     adaptive_info = None
     if batched_adaptive:   # untimed: rays of the adaptive passes (selection depends on the primary images)
         ast, nsel = adaptive_frames(prims[0], bufs, F, True, stream)
-        rays_timed_local += n_full * rays_of(ast) + (rays_of(adaptive_frames(prims[0], bufs, rem, True, stream)[0])
-                                                     if rem else 0)
+        rays_adaptive_local += n_full * rays_of(ast) + (rays_of(adaptive_frames(prims[0], bufs, rem, True, stream)[0])
+                                                        if rem else 0)
         rays_frame0_local += rays_of(adaptive_frames(prims[0], bufs, 1, True, stream)[0])
         adaptive_info = {"pixels_supersampled_per_frame": round(nsel / F, 1), "subp": 4, "threshold": 0.02,
                          "rays_per_frame": round(rays_of(ast) / F, 1), "frames_per_launch": F}
     elif a.adaptive:
         gpu.launch(p64s[0], prims[0][0].data_ptr(), stats=True, stream=stream)
         ast, nsel = adaptive_pass(prims[0][0], bufs[0], True, stream)
-        rays_timed_local += a.steps * rays_of(ast)
+        rays_adaptive_local += a.steps * rays_of(ast)
         rays_frame0_local += rays_of(ast)
         adaptive_info = {("pixels_supersampled" if n == 1 else "pixels_supersampled_rank0"): nsel, "subp": 4,
                          "threshold": 0.02, "rays": rays_of(ast)}
@@ -448,7 +461,8 @@ def main():
                 gstarts.append(g0)
                 gends.append(g1)
 
-    def run(steps, timed, per_launch=F, flags=0):
+    def run(steps, timed, per_launch=None, flags=0):
+        per_launch = per_launch or per_launch_of(assembly)
         li, done = 0, 0
         while done < steps:
             nf = min(per_launch, steps - done)
@@ -482,6 +496,12 @@ def main():
         g_ms = float(np.mean([s_.elapsed_time(e_) for s_, e_ in zip(gstarts, gends)])) if gstarts else 0.0
         return el, k_ms, g_ms
 
+    def same_frames(x, y):
+        """Bitwise equality of two assembled launches' frames (rank 0), over the frames both
+        rendered: a launch of nf frames renders views cams[:nf]."""
+        k = min(x.shape[0], y.shape[0])
+        return torch.equal(x[:k], y[:k])
+
     def choose_assembly():
         """--assembly auto (N > 1): both assemblies render the same two launches of F frames (after one
         warm-up launch each, untimed for the result); peer wins if it was faster and its frames equal the
@@ -503,7 +523,7 @@ def main():
             run(F, False)
             secs[mode] = timed_region(lambda: run(2 * F, False))
             frames[mode] = image.clone() if rank == 0 else None
-        same = torch.tensor([float(torch.equal(frames["gather"], frames["peer"])) if rank == 0 else 0.0],
+        same = torch.tensor([float(same_frames(frames["gather"], frames["peer"])) if rank == 0 else 0.0],
                             dtype=torch.float64, device="cuda")
         dist.broadcast(same, src=0)
         identical = bool(same[0] == 1.0)
@@ -515,6 +535,7 @@ def main():
     assembly_choice = None
     if assembly == "auto":
         assembly, assembly_choice = choose_assembly()
+    rays_timed_local = rays_timed_for(per_launch_of(assembly)) + rays_adaptive_local
     elapsed, kernel_ms_avg, gather_ms_avg = timed_run(a.warmup)
     frames_per_launch = float(np.mean(launch_frames))
     last_image = image
@@ -587,15 +608,18 @@ def main():
         assembly = "peer" if main_as == "gather" else "gather"
         el2, k2, g2 = timed_run(min(a.warmup, F))
         (el2_max, _), (k2_max, _), (g2_max, g2_r0) = over_ranks([el2, k2, g2])
-        same = torch.tensor([1.0 if rank != 0 else float(torch.equal(image, main_frames))], dtype=torch.float64,
-                            device="cuda")
+        same = torch.tensor([1.0 if rank != 0 else float(same_frames(image, main_frames)),
+                             rays_timed_for(per_launch_of(assembly))], dtype=torch.float64, device="cuda")
         if n > 1:
-            dist.broadcast(same, src=0)
+            dist.broadcast(same[:1], src=0)
+            dist.all_reduce(same[1:], op=dist.ReduceOp.SUM)
+        rays_other = float(same[1])
         multi["assembly_ab"] = {
             main_as: {"value": round(rays_total / elapsed / 1e6, 2), "ms_per_step": round(elapsed / a.steps * 1e3, 4),
                       "render_ms_per_launch_max": multi["render_ms_per_launch_max"],
                       "gather_ms_per_launch_rank0": multi["gather_ms_per_launch_rank0"]},
-            assembly: {"value": round(rays_total / el2_max / 1e6, 2), "ms_per_step": round(el2_max / a.steps * 1e3, 4),
+            assembly: {"value": round(rays_other / el2_max / 1e6, 2), "ms_per_step": round(el2_max / a.steps * 1e3, 4),
+                       "frames_per_launch": per_launch_of(assembly),
                        "render_ms_per_launch_max": round(k2_max, 4), "gather_ms_per_launch_rank0": round(g2_r0, 4)},
             "frames_identical": bool(same[0] == 1.0)}
         assembly = main_as

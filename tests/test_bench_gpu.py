@@ -21,14 +21,16 @@ def _gpu(gpu_available):
 SWEEP = 0.12
 
 
-def expected_frames(w, h, frames):
-    """The bench's animation path (rtamd.camera_orbit over each launch's frames): the last
-    frame it saves and the mean rays per frame of one launch, rendered here directly."""
+def expected_frames(w, h, frames, upto=None):
+    """The bench's animation path (rtamd.camera_orbit over the F = `frames` views of a launch): the
+    last frame of a launch of the first `upto` views (default all) -- the frame it saves -- and the
+    mean rays per frame of that launch, rendered here directly."""
     hs = rtamd.HostScene.generate("office")
     hs.prepare()
     dev = rtamd.DeviceScene(hs, 0)
     p = hs.render_params(w, h, 1)
     cams = [rtamd.camera_orbit(p, SWEEP * (f / (frames - 1) - 0.5)) for f in range(frames)] if frames > 1 else [p]
+    cams = cams[:upto or len(cams)]
     rays, img = 0, None
     for c in cams:
         img, st = dev.render(c)
@@ -165,7 +167,10 @@ def test_bench_four_ranks_driver_shape(tmp_path):
                        capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     d = json.loads(r.stdout.strip().splitlines()[-1])
-    assert d["n_gpus"] == 4 and d["config"]["frames_per_launch"] == 10 and d["steps"] == 20
+    # the orbit spans F = 20 views; the gather renders them 10 per launch (two launches), the peer
+    # assembly 20 per launch (one)
+    fpl = d["config"]["frames_per_launch"]
+    assert d["n_gpus"] == 4 and d["steps"] == 20 and fpl == (10 if d["multi_gpu"]["assembly"] == "gather" else 20)
     # the N > 1 instrumentation: render and gather time per launch (max over ranks), and the run
     # again with 32 CUs reserved for the gather (reserve_cus 0 is the default)
     m = d["multi_gpu"]
@@ -184,6 +189,7 @@ def test_bench_four_ranks_driver_shape(tmp_path):
     asm = m["assembly_ab"]
     other = "peer" if m["assembly"] == "gather" else "gather"
     assert asm["frames_identical"] is True and asm[m["assembly"]]["value"] == d["value"] and asm[other]["value"] > 0
-    ref, rays = expected_frames(320, 180, 10)
+    assert asm[other]["frames_per_launch"] == (10 if other == "gather" else 20)
+    ref, rays = expected_frames(320, 180, 20, upto=int(fpl))
     assert np.array_equal(np.load(out), ref)
     assert d["config"]["rays_per_frame"] == rays
