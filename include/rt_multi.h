@@ -36,6 +36,15 @@ int rt_multi_create(const rt_scene_soa* soa, const rt_bvh_soa* bvh, const int* d
 /* Number of GPUs of the driver. */
 int rt_multi_device_count(const rt_multi* m);
 
+/* Frame assembly of rt_multi_render*: RT_MULTI_GATHER (default) = one grouped ncclGather per
+ * batch of frames to devices[0] and a re-interleave kernel there; RT_MULTI_PEER = every GPU's
+ * launch writes its stripes straight into the output frames on devices[0] over xGMI
+ * (RT_FLAG_GLOBAL_ROWS), with no copy and no re-interleave.  Setting RT_MULTI_PEER checks and
+ * enables peer access from every device to devices[0]; it fails (RT_ERR_UNSUPPORTED, the
+ * driver unchanged) when a device cannot access it. */
+enum { RT_MULTI_GATHER = 0, RT_MULTI_PEER = 1 };
+int rt_multi_set_assembly(rt_multi* m, int assembly);
+
 /* Renders one whole frame (rt_multi_render_frames with one frame; p->row_begin / row_end / stripe_* are ignored: every row is
  * rendered, sharded as above with the given stripe_height >= 1) into d_out, a DEVICE
  * buffer on devices[0] holding height x width x 3 values of p->out_format, row-major,

@@ -1,5 +1,6 @@
 // rt_multi.hip — single-process multi-GPU driver (include/rt_multi.h): row stripes per GPU,
-// one RCCL gather to devices[0], a re-interleave kernel there.  SURVEY §8(e).
+// one RCCL gather to devices[0], a re-interleave kernel there (or, RT_MULTI_PEER, every GPU storing
+// its rows straight into devices[0]'s frames).  SURVEY §8(e).
 // Frames go in batches (one rt_launch_frames per GPU per batch, so the per-launch drain is paid
 // once per batch), and two batches are in flight: batch i + 1 renders on the other slot's
 // streams while batch i's gather and re-interleave drain.
@@ -101,6 +102,7 @@ struct Slot {
 
 struct rt_multi {
   int n = 0;
+  int assembly = RT_MULTI_GATHER;
   std::vector<int> devices;
   std::vector<rt_scene*> scenes;
   Slot slot[kSlots];
@@ -210,6 +212,68 @@ int rt_multi_create(const rt_scene_soa* soa, const rt_bvh_soa* bvh, const int* d
 
 int rt_multi_device_count(const rt_multi* m) { return m ? m->n : 0; }
 
+int rt_multi_set_assembly(rt_multi* m, int assembly) {
+  if (!m || (assembly != RT_MULTI_GATHER && assembly != RT_MULTI_PEER))
+    return fail(RT_ERR_INVALID, "rt_multi_set_assembly: bad argument");
+  if (assembly == RT_MULTI_PEER)
+    for (int g = 1; g < m->n; ++g) {   // kernels on devices[g] store into devices[0]'s frames
+      int can = 0;
+      HIP_TRY(hipDeviceCanAccessPeer(&can, m->devices[g], m->devices[0]));
+      if (!can)
+        return fail(RT_ERR_UNSUPPORTED, "rt_multi_set_assembly: device " + std::to_string(m->devices[g]) +
+                                            " cannot access device " + std::to_string(m->devices[0]));
+      HIP_TRY(hipSetDevice(m->devices[g]));
+      const hipError_t e = hipDeviceEnablePeerAccess(m->devices[0], 0);
+      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+        return fail(RT_ERR_HIP, std::string("hipDeviceEnablePeerAccess: ") + hipGetErrorString(e));
+      (void)hipGetLastError();
+    }
+  m->assembly = assembly;
+  return RT_OK;
+}
+
+namespace {
+// RT_MULTI_PEER: GPU g renders its stripes of every frame at their global rows of d_outs (devices[0]
+// memory) -- launches of up to RT_MAX_FRAMES frames, all GPUs at once; the call returns when every
+// GPU's launches have ended (each wave released its stores at system scope before it exited).
+int render_frames_peer(rt_multi* m, const rt_render_params* p, int n_frames, int stripe_height, void* const* d_outs,
+                       rt_stats* stats) {
+  const int n = m->n, H = p->camera.height;
+  std::vector<rt_render_params> q(RT_MAX_FRAMES);
+  std::vector<void*> outs(RT_MAX_FRAMES);
+  for (int f0 = 0; f0 < n_frames; f0 += RT_MAX_FRAMES) {
+    const int F = std::min(RT_MAX_FRAMES, n_frames - f0);
+    for (int g = 0; g < n; ++g) {
+      for (int f = 0; f < F; ++f) {
+        q[f] = p[f0 + f];
+        q[f].row_begin = 0;
+        q[f].row_end = H;
+        q[f].stripe_height = stripe_height;
+        q[f].stripe_count = n;
+        q[f].stripe_index = g;
+        q[f].flags |= RT_FLAG_GLOBAL_ROWS;
+        outs[f] = d_outs[f0 + f];
+      }
+      rt_stats st;
+      if (rt_launch_frames(m->scenes[g], q.data(), F, outs.data(), stats ? &st : nullptr, m->slot[0].streams[g]) != RT_OK)
+        return fail(RT_ERR_HIP, std::string("rt_multi_render_frames: device ") + std::to_string(m->devices[g]) +
+                                    ": " + rt_last_error());
+      if (stats) {
+        stats->primary_rays += st.primary_rays;
+        stats->shadow_rays += st.shadow_rays;
+        stats->reflection_rays += st.reflection_rays;
+        stats->pixels += st.pixels;
+      }
+    }
+  }
+  for (int g = 0; g < n; ++g) {
+    HIP_TRY(hipSetDevice(m->devices[g]));
+    HIP_TRY(hipStreamSynchronize(m->slot[0].streams[g]));
+  }
+  return RT_OK;
+}
+}  // namespace
+
 // Largest batch: frames per launch bounded by RT_MAX_FRAMES and by the gathered array on
 // devices[0] (n x frames x shard bytes per slot, at most 8 GB of its 288 GB).
 static int batch_cap(int n, size_t shard_bytes) {
@@ -230,6 +294,13 @@ int rt_multi_render_frames(rt_multi* m, const rt_render_params* p, int n_frames,
     if (!d_outs[f]) return fail(RT_ERR_INVALID, "rt_multi_render_frames: null output buffer");
     if (p[f].camera.width != W || p[f].camera.height != H || p[f].out_format != p->out_format)
       return fail(RT_ERR_INVALID, "rt_multi_render_frames: frames must share size and format");
+  }
+  if (m->assembly == RT_MULTI_PEER) {
+    if (stats) std::memset(stats, 0, sizeof *stats);
+    const auto t0 = std::chrono::steady_clock::now();
+    const int rc = render_frames_peer(m, p, n_frames, stripe_height, d_outs, stats);
+    if (ms) *ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return rc;
   }
   const int elem = p->out_format == RT_OUT_RGB_F64 ? 8 : 4;
   const int mr = max_rows_of(H, stripe_height, n);

@@ -7,8 +7,9 @@
 //
 //   rt_render --scene office|cornell|random_tris|spheres|path.sce
 //             [--width W --height H --spp N --max-depth D --tris N --seed S
-//              --detail K --device I --gpus N --frames F --out image.ppm]
-// --gpus N renders each frame on GPUs 0..N-1 (row stripes + one RCCL gather, rt_multi.h);
+//              --detail K --device I --gpus N --assembly gather|peer --frames F --out image.ppm]
+// --gpus N renders each frame on GPUs 0..N-1 (row stripes + one RCCL gather, rt_multi.h; with
+// --assembly peer every GPU stores its rows straight into device 0's frame instead);
 // without it one device (--device) renders through rt_launch_compute_image.
 #include <chrono>
 #include <cstdio>
@@ -31,7 +32,7 @@ class Raytracer {
     rt_host_free(host_);
   }
   // Raytracer::init_cuda equivalent; gpus >= 1: every frame sharded over GPUs 0..gpus-1.
-  bool init(const std::string& scene, const rt_gen_params& gp, int device, int gpus) {
+  bool init(const std::string& scene, const rt_gen_params& gp, int device, int gpus, bool peer) {
     int rc = (scene.size() > 4 && scene.substr(scene.size() - 4) == ".sce") ? rt_host_load(scene.c_str(), &host_)
                                                                               : rt_host_generate(scene.c_str(), &gp, &host_);
     if (rc != RT_OK) return error(rt_host_last_error());
@@ -44,7 +45,9 @@ class Raytracer {
       for (int g = 0; g < gpus; ++g) devs[g] = g;
       if (rt_multi_create(rt_host_soa(host_), rt_host_bvh(host_), devs.data(), gpus, nullptr, &multi_) != RT_OK)
         return error(rt_multi_last_error());
-      std::printf("uploaded to %d devices (row stripes of %d rows, RCCL gather to device 0)\n", gpus, kStripe);
+      if (peer && rt_multi_set_assembly(multi_, RT_MULTI_PEER) != RT_OK) return error(rt_multi_last_error());
+      std::printf("uploaded to %d devices (row stripes of %d rows, %s)\n", gpus, kStripe,
+                  peer ? "peer stores into device 0's frame" : "RCCL gather to device 0");
       return true;
     }
     if (rt_scene_upload(rt_host_soa(host_), rt_host_bvh(host_), device, &gpu_) != RT_OK) return error(rt_last_error());
@@ -100,6 +103,7 @@ class Raytracer {
 int main(int argc, char** argv) {
   std::string scene = "office", out;
   int width = 0, height = 0, spp = 1, max_depth = -1, device = 0, frames = 1, gpus = 0;
+  std::string assembly = "gather";
   rt_gen_params gp{};
   gp.max_depth = -1;
   for (int i = 1; i < argc; ++i) {
@@ -119,12 +123,14 @@ int main(int argc, char** argv) {
     else if (a == "--device") device = std::atoi(next());
     else if (a == "--frames") frames = std::atoi(next());
     else if (a == "--gpus") gpus = std::atoi(next());
+    else if (a == "--assembly") assembly = next();
     else if (a == "--out") out = next();
     else { std::fprintf(stderr, "unknown option %s\n", a.c_str()); return 2; }
   }
   Raytracer rt;
   if (gpus < 0) { std::fprintf(stderr, "--gpus must be >= 1\n"); return 2; }
-  if (!rt.init(scene, gp, device, gpus)) return 1;
+  if (assembly != "gather" && assembly != "peer") { std::fprintf(stderr, "--assembly must be gather or peer\n"); return 2; }
+  if (!rt.init(scene, gp, device, gpus, assembly == "peer")) return 1;
   if (!rt.compute_image(width, height, spp, max_depth, frames)) return 1;
   if (!out.empty() && !rt.write(out)) return 1;
   return 0;

@@ -490,9 +490,10 @@ def write_ppm(path, img):
 
 class MultiScene:
     """One scene on several GPUs of this node, one process (rt_multi.h): every frame is cut
-    into interleaved row stripes per GPU and assembled on devices[0] by one RCCL gather."""
+    into interleaved row stripes per GPU and assembled on devices[0] by one RCCL gather
+    (assembly="gather") or by every GPU storing its rows into devices[0]'s frames ("peer")."""
 
-    def __init__(self, host_scene, devices=(0,), tree=None, **options):
+    def __init__(self, host_scene, devices=(0,), tree=None, assembly="gather", **options):
         self._h = C.c_void_p()
         devs = (C.c_int * len(devices))(*devices)
         opt = upload_options(tree, **options)
@@ -501,6 +502,15 @@ class MultiScene:
         if rc != RT_OK:
             raise RtError(f"rt_multi_create: {multi_lib().rt_multi_last_error().decode()}")
         self.devices = tuple(devices)
+        modes = {"gather": abi.RT_MULTI_GATHER, "peer": abi.RT_MULTI_PEER}
+        if assembly not in modes:
+            self.close()
+            raise ValueError(f"assembly must be one of {sorted(modes)}")
+        if multi_lib().rt_multi_set_assembly(self._h, modes[assembly]) != RT_OK:
+            err = multi_lib().rt_multi_last_error().decode()
+            self.close()
+            raise RtError(f"rt_multi_set_assembly: {err}")
+        self.assembly = assembly
 
     def render(self, params, stripe_height=16):
         """Synchronous render of the whole frame to host memory -> (image [H, W, 3], Stats, ms)."""

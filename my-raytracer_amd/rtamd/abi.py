@@ -27,6 +27,8 @@ RT_FLAG_COST_ORDER = 32
 RT_FLAG_NATURAL_ORDER = 64
 RT_FLAG_GLOBAL_ROWS = 128
 RT_IPC_HANDLE_BYTES = 64
+RT_MULTI_GATHER = 0
+RT_MULTI_PEER = 1
 
 
 class Material(C.Structure):
@@ -218,6 +220,7 @@ MULTI_SYMBOLS = {
     "rt_multi_create": (C.c_int, [C.POINTER(SceneSoA), C.POINTER(BvhSoA), C.POINTER(C.c_int), C.c_int,
                                   C.POINTER(UploadOptions), C.POINTER(C.c_void_p)]),
     "rt_multi_device_count": (C.c_int, [C.c_void_p]),
+    "rt_multi_set_assembly": (C.c_int, [C.c_void_p, C.c_int]),
     "rt_multi_render": (C.c_int, [C.c_void_p, C.POINTER(RenderParams), C.c_int, C.c_void_p, C.POINTER(Stats),
                                   C.POINTER(C.c_double)]),
     "rt_multi_render_frames": (C.c_int, [C.c_void_p, C.POINTER(RenderParams), C.c_int, C.c_int,

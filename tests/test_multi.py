@@ -99,13 +99,15 @@ def test_multi_driver_one_gpu_equals_single_launch(gpu_available, office, fmt):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("assembly", ["gather", "peer"])
 @pytest.mark.parametrize("nf,w,h,sh", [(5, 320, 180, 16), (2, 97, 61, 4), (1, 64, 48, 8)])
-def test_multi_driver_frames_equal_single_launches(gpu_available, office, nf, w, h, sh):
+def test_multi_driver_frames_equal_single_launches(gpu_available, office, nf, w, h, sh, assembly):
     # Batched multi-GPU entry on the box's one GPU (one RCCL rank): batches of frames, two in
-    # flight on separate streams / communicators, every frame equal to its own single launch.
+    # flight on separate streams / communicators (gather), or the GPU's rows stored straight into
+    # the output frames (peer), every frame equal to its own single launch.
     import torch
     hs, _ = office
-    m = rtamd.MultiScene(hs, devices=(0,))
+    m = rtamd.MultiScene(hs, devices=(0,), assembly=assembly)
     dev = rtamd.DeviceScene(hs, 0)
     base = hs.render_params(w, h, 1)
     base.out_format = rtamd.RT_OUT_RGB_F64
@@ -154,8 +156,9 @@ def _natural(p):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("assembly", ["gather", "peer"])
 @pytest.mark.parametrize("nf", [1, 3])
-def test_multi_driver_two_gpus_equal_single_launch(gpu_available, office, nf):
+def test_multi_driver_two_gpus_equal_single_launch(gpu_available, office, nf, assembly):
     # The N > 1 path proper: grouped ncclGather of several GPUs' padded stripe buffers,
     # per-device streams, re-interleave on devices[0].  Needs a multi-GPU node (the one-GPU
     # box skips it; INTEGRATION.md "Verification status of the N > 1 path").
@@ -165,7 +168,7 @@ def test_multi_driver_two_gpus_equal_single_launch(gpu_available, office, nf):
         pytest.skip("needs >= 2 GPUs")
     hs, _ = office
     devs = tuple(range(min(n, 8)))
-    m = rtamd.MultiScene(hs, devices=devs)
+    m = rtamd.MultiScene(hs, devices=devs, assembly=assembly)
     dev = rtamd.DeviceScene(hs, 0)
     base = hs.render_params(160, 97, 1)
     base.out_format = rtamd.RT_OUT_RGB_F64
@@ -183,6 +186,13 @@ def test_multi_driver_two_gpus_equal_single_launch(gpu_available, office, nf):
 
 
 @pytest.mark.gpu
+def test_multi_driver_rejects_unknown_assembly(gpu_available, office):
+    hs, _ = office
+    with pytest.raises(ValueError):
+        rtamd.MultiScene(hs, devices=(0,), assembly="scatter")
+
+
+@pytest.mark.gpu
 def test_multi_driver_rejects_duplicate_devices(gpu_available, office):
     hs, _ = office
     with pytest.raises(rtamd.RtError, match="distinct"):
@@ -190,14 +200,15 @@ def test_multi_driver_rejects_duplicate_devices(gpu_available, office):
 
 
 @pytest.mark.gpu
-def test_cli_gpus_path_pixels(gpu_available, tmp_path, office):
+@pytest.mark.parametrize("assembly", ["gather", "peer"])
+def test_cli_gpus_path_pixels(gpu_available, tmp_path, office, assembly):
     hs, orc = office
     out = tmp_path / "m.ppm"
     r = subprocess.run([str(ROOT / "my-raytracer_amd/bin/rt_render"), "--scene", "office", "--width", "96",
-                        "--height", "54", "--gpus", "1", "--out", str(out)], capture_output=True, text=True,
-                       timeout=300)
+                        "--height", "54", "--gpus", "1", "--assembly", assembly, "--out", str(out)],
+                       capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
-    assert "RCCL gather" in r.stdout and "Mrays/s" in r.stdout
+    assert ("RCCL gather" if assembly == "gather" else "peer stores") in r.stdout and "Mrays/s" in r.stdout
     data = out.read_bytes()
     head = b"P6\n96 54\n255\n"
     assert data.startswith(head)
