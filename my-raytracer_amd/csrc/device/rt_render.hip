@@ -68,17 +68,13 @@ constexpr int kCtrWords = 40;       // [8,16) stats (STATS variants), [16,40) di
 // deeper entries spill to a per-lane global array.  Bounds LDS per block independently
 // of tree depth, so occupancy stays VGPR-limited.
 constexpr int kShortStack = 8;
-#ifndef RT_COOP
-#define RT_COOP 2   // nodes per wave's stage of the cooperative node fetch (below); 0 = off
-#endif
 // Top treelet in LDS: the first kTopNodes 4-wide nodes (breadth-first numbering) are copied
 // into each block's LDS; a node iteration whose active lanes all sit in the treelet reads
 // LDS instead of the vector-L1 path.  0 disables.
 // LDS per thread: kSlotDoubles fp64 slot words, task + visibility words, the stack ring
 constexpr int kSlotDoubles = 10;
 // fills the CU's 160 KB at 4 blocks with the slots, ring, lights, pool (73 nodes)
-constexpr int kTopNodes = (40960 - kBlock * (kSlotDoubles * 8 + (2 + kShortStack) * 4) - RT_MAX_LIGHTS * 48 - 64 -
-                           (kBlock / 64) * RT_COOP * 144) / 128;
+constexpr int kTopNodes = (40960 - kBlock * (kSlotDoubles * 8 + (2 + kShortStack) * 4) - RT_MAX_LIGHTS * 48 - 64) / 128;
 constexpr int kStackMask = kShortStack - 1;
 // Tail compaction: once the work queue is empty, a wave with at most kDonateMax
 // pixels in flight hands them to the other waves of its block and exits, so the last pixels
@@ -89,15 +85,6 @@ constexpr int kDonateMax = 24;   // (0 = tail compaction off: -2.8 % batched, -1
 constexpr int kMigWords = 8;
 static_assert(kMigWords <= kShortStack, "migration words travel in the stack ring entries");
 constexpr int kPoolBytes = 64;   // LDS: live-wave count, one 64-bit lane mask per wave of the block, exhausted heads
-// Cooperative node fetch (round 5): a global 4-wide node iteration whose active lanes visit at most
-// kCoop distinct nodes, each by at least kCoopMin lanes, loads every node once -- the lanes of a
-// node each load 16 B of it (1-2 wave-level loads instead of 7) into the wave's LDS stage -- and
-// reads it from there like the treelet.  The stage (kCoop nodes per wave, 144-B stride: the slots'
-// 16-B chunks fall on different banks) comes out of the treelet's share of the block's 40 KB.
-constexpr int kCoop = RT_COOP;
-constexpr int kCoopMin = 4;
-constexpr int kStageStride = 144;
-constexpr int kStageBytes = (kBlock / 64) * kCoop * kStageStride;
 static_assert(8 + 8 * (kBlock / 64) + 4 <= kPoolBytes, "compaction pool does not fit");
 static_assert((kShortStack & kStackMask) == 0, "the stack ring must be a power of two");
 
@@ -278,7 +265,6 @@ struct KParams {
   int n_frames;
   int lights_off;           // LDS byte offset of the lights copy ([n_lights][6] doubles)
   int pool_off;             // LDS byte offset of the compaction pool (kPoolBytes)
-  int stage_off;            // LDS byte offset of the waves' node stages (kStageBytes)
   long long frame_tiles;
   const FrameDesc* frames;  // [n_frames]
   // tile order (RT_FLAG_COST_ORDER): work item w belongs to linear tile tile_order[w / 64] instead of
@@ -1259,58 +1245,13 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
               const uint32_t c0 = __shfl(cur, __ffsll((long long)wballot(1)) - 1);
               if (wballot(cur != c0) == 0) wave_tick(d_gn_uni, d_dummy, lane);
             }
-            bool coop = false;
-            uint32_t c_slot = 0, c_rank = 0, c_size = 1;
-            if constexpr (kCoop > 0) {
-              // the distinct nodes of the active lanes, up to kCoop (wave-uniform loop)
-              unsigned long long todo = wballot(true);
-              int minsz = 64;
-#pragma unroll
-              for (int sl = 0; sl < kCoop; ++sl) {
-                if (todo != 0ull) {
-                  const int l = (int)__builtin_ctzll(todo);
-                  const uint32_t nd = (uint32_t)__builtin_amdgcn_readlane((int)cur, l);
-                  const unsigned long long m = wballot(cur == nd);
-                  const int sz = (int)__popcll(m);
-                  if (cur == nd) {
-                    c_slot = (uint32_t)sl;
-                    c_rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                    c_size = (uint32_t)sz;
-                  }
-                  minsz = sz < minsz ? sz : minsz;
-                  todo &= ~m;
-                }
-              }
-              coop = todo == 0ull && minsz >= kCoopMin;   // wave-uniform
-            }
-            if (coop) {
-              // the node's lanes load its 7 chunks (planes 0..95, refs 96..111) into the stage, then
-              // every lane reads its planes from there (kCoopMin >= 4: at most 2 loads per lane)
-              const int wib = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-              unsigned char* stg = lds_raw + P.stage_off + ((uint32_t)wib * kCoop + c_slot) * kStageStride;
-              if (c_rank < 7u)
-                *reinterpret_cast<float4*>(stg + c_rank * 16u) = *reinterpret_cast<const float4*>(RT_NODE_AT(c_rank * 16u));
-              const uint32_t c2 = c_rank + c_size;
-              if (c2 < 7u)
-                *reinterpret_cast<float4*>(stg + c2 * 16u) = *reinterpret_cast<const float4*>(RT_NODE_AT(c2 * 16u));
-              wave_lds_sync();
-              nx = *reinterpret_cast<const float4*>(stg + nxo);
-              fx = *reinterpret_cast<const float4*>(stg + (nxo ^ 16u));
-              ny = *reinterpret_cast<const float4*>(stg + nyo);
-              fy = *reinterpret_cast<const float4*>(stg + (nyo ^ 16u));
-              nz = *reinterpret_cast<const float4*>(stg + nzo);
-              fz = *reinterpret_cast<const float4*>(stg + (nzo ^ 16u));
-              rf = *reinterpret_cast<const uint4*>(stg + 96);
-              wave_lds_sync();   // the stage is rewritten by the wave's next cooperative iteration
-            } else {
-              nx = *reinterpret_cast<const float4*>(RT_NODE_AT(nxo));
-              fx = *reinterpret_cast<const float4*>(RT_NODE_AT(nxo ^ 16u));
-              ny = *reinterpret_cast<const float4*>(RT_NODE_AT(nyo));
-              fy = *reinterpret_cast<const float4*>(RT_NODE_AT(nyo ^ 16u));
-              nz = *reinterpret_cast<const float4*>(RT_NODE_AT(nzo));
-              fz = *reinterpret_cast<const float4*>(RT_NODE_AT(nzo ^ 16u));
-              rf = *reinterpret_cast<const uint4*>(RT_NODE_AT(96u));
-            }
+            nx = *reinterpret_cast<const float4*>(RT_NODE_AT(nxo));
+            fx = *reinterpret_cast<const float4*>(RT_NODE_AT(nxo ^ 16u));
+            ny = *reinterpret_cast<const float4*>(RT_NODE_AT(nyo));
+            fy = *reinterpret_cast<const float4*>(RT_NODE_AT(nyo ^ 16u));
+            nz = *reinterpret_cast<const float4*>(RT_NODE_AT(nzo));
+            fz = *reinterpret_cast<const float4*>(RT_NODE_AT(nzo ^ 16u));
+            rf = *reinterpret_cast<const uint4*>(RT_NODE_AT(96u));
 #undef RT_NODE_AT
           }
 #pragma unroll
@@ -2111,8 +2052,7 @@ size_t lds_bytes(int /*stack_words*/, int ring = kShortStack) {
 }
 // ... plus the top treelet (n_top 128-B nodes) after it
 size_t lds_bytes_total(int stack_words, int n_top, int ring = kShortStack) {
-  return lds_bytes(stack_words, ring) + (size_t)n_top * sizeof(GNode4) + RT_MAX_LIGHTS * 6 * sizeof(double) + kPoolBytes +
-         kStageBytes;
+  return lds_bytes(stack_words, ring) + (size_t)n_top * sizeof(GNode4) + RT_MAX_LIGHTS * 6 * sizeof(double) + kPoolBytes;
 }
 // treelet nodes that fit next to a ring of the given size in a block's 40 KB (kTopNodes beside the
 // 8-entry ring)
@@ -2735,7 +2675,6 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   P.top_off = (int)lds_bytes(sc->stack_words, ring);
   P.lights_off = P.top_off + n_top * (int)sizeof(GNode4);
   P.pool_off = P.lights_off + RT_MAX_LIGHTS * 6 * (int)sizeof(double);
-  P.stage_off = P.pool_off + kPoolBytes;
   const long long waves_needed = (P.n_tiles * 64 + 63) / 64;
   int bpc = sc->blocks_per_cu[v];
   if (sc->bpc_cap > 0) bpc = std::min(bpc, sc->bpc_cap);   // a smaller persistent grid (upload option)
