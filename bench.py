@@ -603,7 +603,10 @@ def main():
 
     # N > 1: the same run with the other frame assembly (RCCL gather <-> peer stores + fence), and
     # the last launch's assembled frames compared bit for bit with the main run's (same views)
-    if multi is not None and (a.assembly_ab == "on" or (a.assembly_ab == "auto" and not a.adaptive)):
+    peer_failed = bool(assembly_choice and assembly_choice.get("reason"))
+    if peer_failed:
+        multi["assembly_ab"] = {"skipped": assembly_choice["reason"]}
+    elif multi is not None and (a.assembly_ab == "on" or (a.assembly_ab == "auto" and not a.adaptive)):
         main_as = assembly
         assembly = "peer" if main_as == "gather" else "gather"
         el2, k2, g2 = timed_run(min(a.warmup, F))
@@ -632,16 +635,29 @@ def main():
         main_r = multi["reserve_cus"]
         other = 32 if main_r <= 0 else 0
         gpu.close()
-        gpu = rtamd.DeviceScene(host, device=dev, analytic=a.analytic or a.scene == "spheres", tree=a.tree,
-                                **dict(upload_opts, reserve_cus=other))
-        el2, k2, g2 = timed_run(min(a.warmup, F))
-        (el2_max, _), (k2_max, _), (g2_max, g2_r0) = over_ranks([el2, k2, g2])
-        rec = {str(main_r): {"value": round(rays_total / elapsed / 1e6, 2), "ms_per_step": round(elapsed / a.steps * 1e3, 4),
-                             "render_ms_per_launch_max": multi["render_ms_per_launch_max"],
-                             "gather_ms_per_launch_rank0": multi["gather_ms_per_launch_rank0"]},
-               str(other): {"value": round(rays_total / el2_max / 1e6, 2), "ms_per_step": round(el2_max / a.steps * 1e3, 4),
-                            "render_ms_per_launch_max": round(k2_max, 4), "gather_ms_per_launch_rank0": round(g2_r0, 4)}}
-        multi["reserve_cus_ab"] = rec
+        err = ""
+        try:   # the CU-masked streams are created (and their masks read back) at the first launch
+            gpu = rtamd.DeviceScene(host, device=dev, analytic=a.analytic or a.scene == "spheres", tree=a.tree,
+                                    **dict(upload_opts, reserve_cus=other))
+            gpu.launch(cams[0], bufs[0].data_ptr(), stats=False, stream=stream)
+            torch.cuda.synchronize()
+        except Exception as e:   # every rank learns of it before any further collective
+            err = repr(e)
+        ok = torch.tensor([0.0 if err else 1.0], dtype=torch.float64, device="cuda")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if ok[0] < 1.0:
+            multi["reserve_cus_ab"] = {"skipped": f"reserve_cus {other} failed" +
+                                                  (f" here: {err}" if err else " on another rank")}
+        else:
+            el2, k2, g2 = timed_run(min(a.warmup, F))
+            (el2_max, _), (k2_max, _), (g2_max, g2_r0) = over_ranks([el2, k2, g2])
+            multi["reserve_cus_ab"] = {
+                str(main_r): {"value": round(rays_total / elapsed / 1e6, 2), "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+                              "render_ms_per_launch_max": multi["render_ms_per_launch_max"],
+                              "gather_ms_per_launch_rank0": multi["gather_ms_per_launch_rank0"]},
+                str(other): {"value": round(rays_total / el2_max / 1e6, 2),
+                             "ms_per_step": round(el2_max / a.steps * 1e3, 4),
+                             "render_ms_per_launch_max": round(k2_max, 4), "gather_ms_per_launch_rank0": round(g2_r0, 4)}}
 
     if rank == 0:
         if a.save:
