@@ -30,6 +30,7 @@ def main(src, dst):
             "frames_per_launch": d["config"]["frames_per_launch"], "rays_per_frame": d["config"]["rays_per_frame"],
             "single_frame_ms": sf.get("ms_per_frame"),
             "roofline_frac": (d.get("roofline") or {}).get("frac"),
+            "bound": (d.get("roofline") or {}).get("bound"),
             "cpu_mrays_s": cb.get("value"), "cpu_threads": cb.get("cores"), "cpu_frame_s": cb.get("frame_s"),
             "cpu_frame_s_extrapolated": cb.get("frame_s_extrapolated"), "cpu_sample": cb.get("sample"),
             "gpu_over_cpu": round(d["value"] / cb["value"], 1) if cb.get("value") else None,
