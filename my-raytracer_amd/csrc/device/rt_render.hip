@@ -2687,17 +2687,11 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
 
   // the context's previous launch done (device side) and its staged copy consumed (host side); a
   // launch eight back has normally ended, and then no wait goes into the stream
-#ifdef RT_LAUNCH_SEPARATE_EVENTS   // A/B: rounds 1-4's launch sequence
-  if (C.used) {
-    HIP_TRY(hipStreamWaitEvent(st, C.ev1, 0));
-    HIP_TRY(hipEventSynchronize(C.ev1));
-  }
-#else
+  // (with the events below: one frame per call 0.4130 -> 0.4089 ms kernel, 0.4295 -> 0.4265 ms call; r05p)
   if (C.used && hipEventQuery(C.ev1) != hipSuccess) {
     HIP_TRY(hipStreamWaitEvent(st, C.ev1, 0));
     HIP_TRY(hipEventSynchronize(C.ev1));
   }
-#endif
   // zeroed counters + frame table, one copy from the context's pinned staging
   std::memset(C.h_ctl, 0, kCtrBytes);
   FrameDesc* fd = reinterpret_cast<FrameDesc*>(C.h_ctl + kCtrBytes);
@@ -2719,15 +2713,6 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
     HIP_TRY(hipMemsetAsync(C.d_tl, 0, tb, st));
   }
   P.tl = C.d_tl;
-#ifdef RT_LAUNCH_SEPARATE_EVENTS
-  HIP_TRY(hipEventRecord(C.ev0, st));
-  if (rows > 0) {
-    void* args[] = {&P};
-    HIP_TRY(hipLaunchKernel(reinterpret_cast<const void*>(kVariants[v].fn), dim3((unsigned)blocks), dim3(kBlock),
-                            args, lds, st));
-  }
-  HIP_TRY(hipEventRecord(C.ev1, st));
-#else
   if (rows > 0) {   // the launch's start / stop events travel with the kernel's dispatch (no marker packets)
     void* args[] = {&P};
     HIP_TRY(hipExtLaunchKernel(reinterpret_cast<const void*>(kVariants[v].fn), dim3((unsigned)blocks), dim3(kBlock),
@@ -2736,7 +2721,6 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
     HIP_TRY(hipEventRecord(C.ev0, st));
     HIP_TRY(hipEventRecord(C.ev1, st));
   }
-#endif
   if (st != caller) HIP_TRY(hipStreamWaitEvent(caller, C.ev1, 0));   // the caller's later work follows the launch
   if (cost_order || cost_debug) {   // this launch read / wrote the maps: the next map launch is fenced on it
     if (!sc->maps_ev) HIP_TRY(hipEventCreateWithFlags(&sc->maps_ev, hipEventDisableTiming));
