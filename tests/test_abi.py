@@ -108,6 +108,25 @@ def test_hip_entry_points_reject_bad_arguments():
     assert lib.rt_rows_in_shard(C.byref(p)) == len(rtamd.shard_rows(100, 16, 3, 1))
 
 
+def test_tile_shape_and_ipc_argument_checks():
+    # no GPU needed: the work tile is a compile-time shape (8 x 8: one wave's 64 pixels), and the
+    # IPC entry points reject null arguments before any HIP call
+    assert rtamd.tile_shape() == (8, 8)
+    lib = rtamd.hip_lib()
+    assert lib.rt_tile_shape(None, None) == abi.RT_ERR_INVALID
+    off = C.c_ulonglong(0)
+    assert lib.rt_ipc_get_handle(None, None, C.byref(off)) == abi.RT_ERR_INVALID
+    assert lib.rt_ipc_open(None, 0, 0, -1, None) == abi.RT_ERR_INVALID
+    assert lib.rt_ipc_close(None, 0) == abi.RT_ERR_INVALID
+    with pytest.raises(ValueError):
+        rtamd.ipc_open(b"short", 0, 0)
+
+
+def test_multi_set_assembly_rejects_bad_arguments():
+    lib = rtamd.multi_lib()
+    assert lib.rt_multi_set_assembly(None, abi.RT_MULTI_PEER) == abi.RT_ERR_INVALID
+
+
 def test_shard_rows_partition_the_image():
     for h, sh, n in [(1080, 16, 8), (1080, 16, 3), (17, 4, 2), (5, 16, 8)]:
         rows = sorted(sum((list(rtamd.shard_rows(h, sh, n, r)) for r in range(n)), []))
