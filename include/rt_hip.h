@@ -184,8 +184,10 @@ int rt_scene_upload(const rt_scene_soa* soa, const rt_bvh_soa* bvh, int device, 
  *   RT_TREE_SAH        binned-SAH tree over all triangles (object splits only), 4-wide collapsed
  *   RT_TREE_REFERENCE  the reference median-split tree, oversize leaves refined */
 enum { RT_TREE_SAH = 0, RT_TREE_REFERENCE = 1, RT_TREE_SBVH = 2 };
-/* 4-wide collapse of the device hierarchy: open the child with the largest box (default), or
- * the SAH-optimal choice of up to 4 slots per node (dynamic programme). */
+/* 4-wide collapse of the device hierarchy: open the child with the largest box, or the
+ * SAH-optimal choice of up to 4 slots per node (dynamic programme; the default).
+ * RT_COLLAPSE_BY_SIZE (the default before round 5: greedy below 2^18 input triangles) now
+ * resolves to RT_COLLAPSE_SAH at every size. */
 enum { RT_COLLAPSE_GREEDY = 0, RT_COLLAPSE_SAH = 1, RT_COLLAPSE_BY_SIZE = 2 };
 
 /* Upload options.  The library reads nothing from the environment: its behaviour depends only
@@ -206,8 +208,7 @@ typedef struct rt_upload_options {
                             device records on, else 8; default), 8 or 16 */
   int lds_treelet;       /* 4-wide nodes each block caches in LDS: 0 = as many as fit (default),
                             > 0 = at most this many, -1 = none */
-  int collapse;          /* RT_COLLAPSE_* (default RT_COLLAPSE_BY_SIZE: SAH from 2^18 input triangles on,
-                            else greedy) */
+  int collapse;          /* RT_COLLAPSE_* (default RT_COLLAPSE_SAH; RT_COLLAPSE_BY_SIZE resolves to it) */
   int sbvh_leaf_max;     /* SBVH: SAH-terminated leaves of up to this many references, 1..8 (1 = split
                             down to single references); 0 = by size (default): 1 from 2^18 input
                             triangles on, else 2 */

@@ -897,11 +897,14 @@ int validate(const rt_scene_soa* s, const rt_bvh_soa* b) {
 // kSbvhLeafBySize triangles on (random soups, config 4) single-reference leaves, the SAH-optimal
 // collapse and spatial splits wherever they pay (alpha 0, budget 1.5): 10 M random triangles
 // 4722 -> 4804 Mrays/s for the last three (profiles/r03/r03zl_ab_rt10m_tree.txt); below it the
-// office's tuning (leaves of up to 2, greedy collapse, alpha 1e-5, budget 0.75).
+// office's tuning (leaves of up to 2, alpha 1e-5, budget 0.75).  The SAH-optimal collapse is the
+// default at every size since round 5 (office one frame -1.5 %, batched -0.9 %,
+// profiles/r05/r05u_ab_tree_office.txt, r05v_ab_collapse_office.txt); RT_COLLAPSE_BY_SIZE, the
+// earlier default, resolves to it as well.
 static rt_upload_options options_by_size(rt_upload_options o, long long nt) {
   const bool deep = nt >= kSbvhLeafBySize;
   if (o.sbvh_leaf_max == 0) o.sbvh_leaf_max = deep ? 1 : 2;
-  if (o.collapse == RT_COLLAPSE_BY_SIZE) o.collapse = deep ? RT_COLLAPSE_SAH : RT_COLLAPSE_GREEDY;
+  if (o.collapse == RT_COLLAPSE_BY_SIZE) o.collapse = RT_COLLAPSE_SAH;
   if (o.sbvh_alpha < 0.0) o.sbvh_alpha = deep ? 0.0 : kSbvhAlpha;
   if (o.sbvh_budget < 0.0) o.sbvh_budget = deep ? 1.5 : kSbvhBudget;
   return o;
@@ -1259,7 +1262,7 @@ void upload_options_defaults(rt_upload_options* o) {
   o->build_threads = 0;
   o->stack_ring = 0;
   o->lds_treelet = 0;   // as many as fit
-  o->collapse = RT_COLLAPSE_BY_SIZE;
+  o->collapse = RT_COLLAPSE_SAH;
   o->sbvh_leaf_max = kSbvhLeafMax;
   o->sbvh_bins = kSbvhBins;
   o->blocks_per_cu = 0;

@@ -79,7 +79,7 @@ def test_upload_options_defaults_and_validation():
     # The library reads no environment: every build / layout choice is an rt_upload_options field.
     o = abi.UploadOptions()
     rtamd.hip_lib().rt_upload_options_init(C.byref(o))
-    assert (o.device_tree, o.stack_ring, o.lds_treelet, o.collapse) == (abi.RT_TREE_SBVH, 0, 0, abi.RT_COLLAPSE_BY_SIZE)
+    assert (o.device_tree, o.stack_ring, o.lds_treelet, o.collapse) == (abi.RT_TREE_SBVH, 0, 0, abi.RT_COLLAPSE_SAH)
     assert (o.sbvh_leaf_max, o.sbvh_bins, o.blocks_per_cu, o.grid_spare, o.verbose) == (0, 32, 0, 0, 0)
     assert (o.sbvh_alpha, o.sbvh_budget, o.sbvh_c_trav, o.collapse_c_tri) == (-1.0, -1.0, 1.0, 1.0)
     assert (o.reserve_cus, o.order_window) == (0, 0)

@@ -16,7 +16,7 @@ gen = {"n_triangles": int(sys.argv[2])} if len(sys.argv) > 2 else {}
 host = rtamd.HostScene.generate(scene, **gen)
 host.prepare()
 opts = dict(kv.split("=") for kv in os.environ.get("RTAMD_AB_OPTS", "").split(",") if kv)
-gpu = rtamd.DeviceScene(host, 0, **{k: int(v) for k, v in opts.items()})
+gpu = rtamd.DeviceScene(host, 0, **{k: (float(v) if "." in v else int(v)) for k, v in opts.items()})
 p = host.render_params(1920, 1080, 1)
 out = [torch.zeros((1080, 1920, 3), device="cuda") for _ in range(64)]
 for _ in range(5):
