@@ -335,18 +335,24 @@ def main():
     n_full, rem = divmod(a.steps, F)
     st = launch_counts(F)
     rays_cache = {}
+    counts_cache = {F: st}   # ray counts of a launch of nf frames (deterministic): one counting launch per shape
+
+    def counts_of(nf):
+        if nf not in counts_cache:
+            counts_cache[nf] = launch_counts(nf)
+        return counts_cache[nf]
 
     def rays_timed_for(pl):
         """This rank's rays in a.steps frames rendered pl at a time (launches of frames cams[:pl])
         -- from untimed counting launches of exactly those shapes."""
         if pl not in rays_cache:
             nf_, rm_ = divmod(a.steps, pl)
-            rays_cache[pl] = nf_ * rays_of(launch_counts(pl)) + (rays_of(launch_counts(rm_)) if rm_ else 0)
+            rays_cache[pl] = nf_ * rays_of(counts_of(pl)) + (rays_of(counts_of(rm_)) if rm_ else 0)
         return rays_cache[pl]
     rays_adaptive_local = 0
     # the single-frame records render frames cams[0 .. NS) one per launch (an animation: distinct views)
     NS = max(1, min(a.single_frames, F))
-    rays_frame0_local = rays_of(launch_counts(NS)) / NS  # rays per frame of those frames
+    rays_frame0_local = rays_of(counts_of(NS)) / NS  # rays per frame of those frames
     tst = launch_counts(F, rtamd.RT_FLAG_TRAVERSAL_STATS)   # canonical 2-wide walk of the reference tree
     wst = launch_counts(F, rtamd.RT_FLAG_WIDE_STATS)        # the production kernel's own fetches
     adaptive_info = None
