@@ -75,7 +75,11 @@ class PeerFrames:
     complete on rank 0 after fence(): a one-element all_reduce on the launch stream of every rank
     (RCCL with "nccl"), which starts after that rank's render in stream order, so rank 0's stream
     passes it only when every rank's render has ended (its waves release their image stores at
-    system scope before they exit).  With frames == 0 the buffers are single images [H, W, C]."""
+    system scope before they exit).  With frames == 0 the buffers are single images [H, W, C].
+    Reuse: a rank's next launch into a slot waits only for that slot's previous fence, not for
+    what rank 0 does with the frames after it -- a consumer on rank 0 (a copy, an encoder) must be
+    done with slot s before any rank launches into s again: give every rank a second fence() after
+    the consumer, or enough slots that the consumer ends first (bench.py consumes nothing)."""
 
     def __init__(self, height, width, n, rank, device, frames=0, slots=1, dtype=torch.float32, channels=3):
         from . import ipc_handle, ipc_open   # librt_hip (lazy: importing this module needs no GPU)
