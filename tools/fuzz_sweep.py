@@ -1,0 +1,90 @@
+"""Extended parity sweep (dev tool, under gpurun): the GPU suite's seeded random scenes
+(tests/fuzz_scenes.py) over many more seeds than the suite runs, each rendered by the production
+kernel and by the CPU oracle (reference CPU semantics, oracle/) and compared -- fp64 pixels within
+1e-12, ray counts exact.  Per seed: the plain mesh scene at an odd image size with 1-3 spp, the
+same scene with spheres and planes (analytic path, CPU intersect_scene semantics) and with a
+textured mesh; every 5th seed also on the SAH and refined-reference device trees (bit-identical
+to the default SBVH).  The oracle here is the checker, never the thing measured.
+
+usage: python tools/fuzz_sweep.py FIRST_SEED N_SEEDS OUT.json
+"""
+import json
+import sys
+import tempfile
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "my-raytracer_amd"))
+sys.path.insert(0, str(ROOT / "oracle"))
+sys.path.insert(0, str(ROOT / "tests"))
+import fuzz_scenes  # noqa: E402
+import pyoracle  # noqa: E402
+import rtamd  # noqa: E402
+
+TOL64 = 1e-12
+
+
+def counts(st):
+    return [st.primary_rays, st.shadow_rays, st.reflection_rays]
+
+
+def check(hs, p, analytic=False, trees=("sbvh",)):
+    """Max |GPU - oracle| over the image and whether every tree gave the same bits and counts."""
+    orc = pyoracle.Oracle(hs.raw, hs)
+    ref, cnt = orc.render(p, pyoracle.MODE_REFERENCE)
+    p.out_format = rtamd.RT_OUT_RGB_F64
+    first = None
+    err, same, rays = 0.0, True, 0
+    for tree in trees:
+        dev = rtamd.DeviceScene(hs, 0, analytic=analytic, tree=tree)
+        img, st = dev.render(p)
+        dev.close()
+        err = max(err, float(np.abs(img - ref).max()))
+        ok_counts = counts(st) == [cnt.primary_rays, cnt.shadow_rays, cnt.reflection_rays]
+        if first is None:
+            first = (img, counts(st))
+        else:
+            same &= bool(np.array_equal(img, first[0]) and counts(st) == first[1])
+        same &= ok_counts
+        rays = sum(counts(st))
+    return err, same, rays
+
+
+def main():
+    s0, n, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3]
+    rows, worst, fails, t0 = [], 0.0, [], time.time()
+    with tempfile.TemporaryDirectory() as td:
+        tmp = Path(td)
+        for seed in range(s0, s0 + n):
+            w, h = 33 + seed % 40, 21 + (seed * 7) % 31        # odd and even sizes, partial tiles
+            spp = 1 + seed % 3
+            trees = ("sbvh", "sah", "reference") if seed % 5 == 0 else ("sbvh",)
+            res = {"seed": seed, "size": [w, h], "spp": spp}
+            for kind, writer, analytic in (("mesh", fuzz_scenes.write, False),
+                                           ("analytic", fuzz_scenes.write_analytic, True),
+                                           ("textured", fuzz_scenes.write_textured, False)):
+                d = tmp / f"{kind}{seed}"
+                d.mkdir()
+                hs = rtamd.HostScene.load(writer(d, seed, w, h))
+                hs.prepare()
+                p = hs.render_params(0, 0, spp if kind == "mesh" else 1)
+                err, same, rays = check(hs, p, analytic, trees if kind == "mesh" else ("sbvh",))
+                ok = err <= TOL64 and same
+                res[kind] = {"max_abs_err": err, "exact_counts_and_trees": same, "rays": rays, "ok": ok}
+                worst = max(worst, err)
+                if not ok:
+                    fails.append((seed, kind))
+            rows.append(res)
+            print(json.dumps(res), flush=True)
+    summary = {"seeds": [s0, s0 + n], "scenes": 3 * n, "failures": fails, "worst_max_abs_err": worst,
+               "tolerance": TOL64, "seconds": round(time.time() - t0, 1)}
+    Path(out).write_text(json.dumps({"summary": summary, "rows": rows}, indent=1))
+    print(json.dumps(summary), flush=True)
+    sys.exit(1 if fails else 0)
+
+
+if __name__ == "__main__":
+    main()
