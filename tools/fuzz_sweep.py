@@ -7,6 +7,10 @@ textured mesh; every 5th seed also on the SAH and refined-reference device trees
 to the default SBVH).  The oracle here is the checker, never the thing measured.
 
 usage: python tools/fuzz_sweep.py FIRST_SEED N_SEEDS OUT.json
+       python tools/fuzz_sweep.py --deep FIRST_SEED N_SEEDS OUT.json
+--deep: generated deep scenes instead -- random-triangle soups of 2^15 .. 2^20 triangles (the
+16-entry stack ring and global spills from 2^18 records on) and cornell boxes of random detail,
+random depth 0-5, at 96 x 64 with 1-2 spp.
 """
 import json
 import sys
@@ -53,7 +57,34 @@ def check(hs, p, analytic=False, trees=("sbvh",)):
     return err, same, rays
 
 
+def deep(s0, n, out):
+    rows, worst, fails, t0 = [], 0.0, [], time.time()
+    sizes = [1 << 15, 1 << 16, 1 << 17, 1 << 18, 1 << 19, 1 << 20]
+    for seed in range(s0, s0 + n):
+        kind = "cornell" if seed % 4 == 3 else "random_tris"
+        gen = {"detail": 1 + seed % 6} if kind == "cornell" else {"n_triangles": sizes[seed % len(sizes)]}
+        hs = rtamd.HostScene.generate(kind, seed=seed, max_depth=seed % 6, **gen)
+        hs.prepare()
+        p = hs.render_params(96, 64, 1 + seed % 2)
+        err, same, rays = check(hs, p, False, ("sbvh", "sah") if seed % 3 == 0 else ("sbvh",))
+        ok = err <= TOL64 and same
+        res = {"seed": seed, "scene": kind, **gen, "depth": seed % 6, "max_abs_err": err,
+               "exact_counts_and_trees": same, "rays": rays, "ok": ok}
+        worst = max(worst, err)
+        if not ok:
+            fails.append(seed)
+        rows.append(res)
+        print(json.dumps(res), flush=True)
+    summary = {"deep": True, "seeds": [s0, s0 + n], "scenes": n, "failures": fails, "worst_max_abs_err": worst,
+               "tolerance": TOL64, "seconds": round(time.time() - t0, 1)}
+    Path(out).write_text(json.dumps({"summary": summary, "rows": rows}, indent=1))
+    print(json.dumps(summary), flush=True)
+    sys.exit(1 if fails else 0)
+
+
 def main():
+    if sys.argv[1] == "--deep":
+        deep(int(sys.argv[2]), int(sys.argv[3]), sys.argv[4])
     s0, n, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3]
     rows, worst, fails, t0 = [], 0.0, [], time.time()
     with tempfile.TemporaryDirectory() as td:
