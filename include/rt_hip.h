@@ -26,6 +26,10 @@
  *    share of the image (the reference only uses device 0, mytracer_gpu.cu:34).
  * All pointers are plain; no torch or HIP types appear in the signatures
  * (streams are passed as void*).
+ * Current device: a call that takes a scene makes the scene's device current on the calling
+ * thread and leaves it so (rt_scene_upload*: `device`; rt_ipc_open: `device`), as the
+ * reference's single-device code assumes; a caller driving several GPUs from one thread sets
+ * its own device again after a call (rt_multi.h does).
  */
 #ifndef RT_HIP_H
 #define RT_HIP_H
