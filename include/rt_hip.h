@@ -346,8 +346,11 @@ int rt_launch_adaptive_shard(rt_scene* scene, const rt_render_params* p, const d
  * Returns the entry count (2 x segments); rows_out may be NULL to query it. */
 int rt_adaptive_halo_rows(const rt_render_params* p, int* rows_out, int cap);
 
-/* Convenience for tests / CLI: renders into a HOST buffer (allocates a device
- * buffer internally, synchronous). */
+/* Renders into a HOST buffer, synchronously (the reference's call pattern: Raytracer::
+ * compute_image_cuda copies every frame back, mytracer.cpp:123-159).  A page-locked, device-mapped
+ * buffer (hipHostMalloc, hipHostRegister, torch pin_memory) is written by the kernel directly over
+ * PCIe as pixels finish; pageable memory goes through a device staging buffer kept by the scene
+ * (allocated on first use, grown as needed, freed by rt_scene_free) and one copy. */
 int rt_render_to_host(rt_scene* scene, const rt_render_params* p, void* host_out, rt_stats* stats);
 
 /* Cross-process access to a device buffer, for one process per GPU (the frame-assembly mode

@@ -250,6 +250,33 @@ def test_deterministic_and_stream_launch():
     assert dev.last_kernel_ms() > 0
 
 
+@pytest.mark.parametrize("fmt", ["f32", "f64"])
+def test_render_to_host_pinned_and_pageable(fmt):
+    # rt_render_to_host: a page-locked caller buffer is written by the kernel directly over PCIe,
+    # pageable memory through the scene's staging buffer (reused, grown for a larger frame); both
+    # give the device-buffer launch's bits and ray counts, over consecutive orbit views (cost-ordered
+    # one-frame launches) and sizes that shrink and grow
+    import ctypes as C
+    import torch
+
+    hs, dev, _ = Case.get("office")
+    lib = rtamd.hip_lib()
+    dt = torch.float64 if fmt == "f64" else torch.float32
+    for k, (w, h) in enumerate([(320, 180), (96, 54), (400, 226), (320, 180)]):
+        p = rtamd.camera_orbit(hs.render_params(w, h, 1), 0.02 * k)
+        p.out_format = rtamd.RT_OUT_RGB_F64 if fmt == "f64" else rtamd.RT_OUT_RGB_F32
+        want = torch.zeros((h, w, 3), dtype=dt, device="cuda")
+        st0 = dev.launch(p, want.data_ptr(), stats=True)
+        pinned = torch.full((h, w, 3), -1.0, dtype=dt).pin_memory()
+        st1 = rtamd.abi.Stats()
+        assert lib.rt_render_to_host(dev._h, C.byref(p), C.c_void_p(pinned.data_ptr()), C.byref(st1)) == 0
+        page, st2 = dev.render(p)   # numpy: pageable
+        ref = want.cpu().numpy()
+        assert np.array_equal(pinned.numpy(), ref), (w, h)
+        assert np.array_equal(page, ref), (w, h)
+        assert counts(st1) == counts(st0) == counts(st2)
+
+
 @pytest.mark.parametrize("nf", [1, 3])
 def test_tile_order_and_costs_change_no_pixel(nf):
     # Work order (rt_debug_set_tile_order: any permutation of the launch's tiles) and the per-tile
