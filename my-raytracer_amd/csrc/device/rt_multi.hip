@@ -107,6 +107,8 @@ struct rt_multi {
   std::vector<rt_scene*> scenes;
   Slot slot[kSlots];
   size_t sbuf_bytes = 0;       // bytes of every slot's per-device stripe buffer
+  void* d_host_stage = nullptr;   // rt_multi_render_to_host: the assembled frame on devices[0], kept
+  size_t host_stage_bytes = 0;
 };
 
 extern "C" {
@@ -154,6 +156,7 @@ void rt_multi_free(rt_multi* m) {
       if (S.h_outs) (void)hipHostFree(S.h_outs);
       if (S.done) (void)hipEventDestroy(S.done);
     }
+    if (m->d_host_stage) (void)hipFree(m->d_host_stage);
   }
   delete m;
 }
@@ -403,18 +406,19 @@ int rt_multi_render_to_host(rt_multi* m, const rt_render_params* p, int stripe_h
   if (!m || !p || !host_out) return fail(RT_ERR_INVALID, "rt_multi_render_to_host: bad argument");
   const size_t bytes = (size_t)p->camera.width * p->camera.height * 3 * (p->out_format == RT_OUT_RGB_F64 ? 8 : 4);
   HIP_TRY(hipSetDevice(m->devices[0]));
-  void* d = nullptr;
-  HIP_TRY(hipMalloc(&d, bytes));
-  const int rc = rt_multi_render(m, p, stripe_height, d, stats, ms);
-  if (rc == RT_OK) {
-    (void)hipSetDevice(m->devices[0]);
-    const hipError_t e = hipMemcpy(host_out, d, bytes, hipMemcpyDeviceToHost);
-    (void)hipFree(d);
-    if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("rt_multi_render_to_host: ") + hipGetErrorString(e));
-    return RT_OK;
+  if (m->host_stage_bytes < bytes) {   // the frame's device buffer, kept between calls (grown as needed)
+    if (m->d_host_stage) HIP_TRY(hipFree(m->d_host_stage));
+    m->d_host_stage = nullptr;
+    m->host_stage_bytes = 0;
+    HIP_TRY(hipMalloc(&m->d_host_stage, bytes));
+    m->host_stage_bytes = bytes;
   }
-  (void)hipFree(d);
-  return rc;
+  const int rc = rt_multi_render(m, p, stripe_height, m->d_host_stage, stats, ms);
+  if (rc != RT_OK) return rc;
+  (void)hipSetDevice(m->devices[0]);
+  const hipError_t e = hipMemcpy(host_out, m->d_host_stage, bytes, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("rt_multi_render_to_host: ") + hipGetErrorString(e));
+  return RT_OK;
 }
 
 }  // extern "C"
