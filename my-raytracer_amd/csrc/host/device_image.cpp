@@ -1115,14 +1115,6 @@ int build_image(const rt_scene_soa* s, const rt_bvh_soa* b, const rt_upload_opti
         g4[n] = (int)order.size();
         order.push_back(n);
         kids.push_back(kids_of(n));
-#if defined(RT_KIDS_ORDER) && RT_KIDS_ORDER > 0
-        {   // A/B: slot order by box area (any-hit waves visit hit children from the last slot down)
-          Kids& k = kids.back();
-          std::stable_sort(k.c, k.c + k.n, [&](int a_, int b_) {
-            return RT_KIDS_ORDER == 1 ? area(a_) < area(b_) : area(a_) > area(b_);
-          });
-        }
-#endif
       };
       assign(0);
       for (size_t q = 0; q < order.size() && (int)order.size() < bfs_top; ++q) {   // breadth-first top
