@@ -1278,8 +1278,8 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
     const uint32_t tv = v[a]; v[a] = v[b]; v[b] = tv;         \
   }
           if (w_any) {   // a wave of any-hit rays: the last hit child first, the others pushed
-            // (a fixed slot order keeps the wave's lanes on the same nodes: orders by ray direction
-            // or by distance lost 2-9 %, the fixed first-slot-first order 4 %)
+            // (orders chosen per lane or per wave from the ray's entry distances lost 2-11 %, the
+            // swaps' cost included; the fixed first-slot-first order 4 %: DESIGN.md §4)
             uint32_t nxt = kDone;
 #pragma unroll
             for (int c = 0; c < 4; ++c)
