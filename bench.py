@@ -18,7 +18,9 @@ are distinct views, and every frame traces all of its rays.  A single_frame reco
 the orbit) is timed after the main run with the library's default for such launches on one
 stream -- cost-ordered work (each launch's work heads take first the tiles that took longest
 two launches before, shortening the drain) -- and beside it
-single_frame.natural_order: the same launches with RT_FLAG_NATURAL_ORDER.  --streams S > 1 keeps S launches in flight on separate streams
+single_frame.natural_order: the same launches with RT_FLAG_NATURAL_ORDER; single_frame.pipelined: the
+same one-frame launches with --pipeline (3) of them in flight on streams of their own (the throughput
+of the reference's call shape for a caller that keeps frames in flight).  --streams S > 1 keeps S launches in flight on separate streams
 (default 1 on one GPU: launches serial, so the HIP-event launch duration is the
 kernel's own duration, as rocprofv3 reports it; 2 on N > 1, so the RCCL gather of
 launch i overlaps launch i+1).
@@ -86,6 +88,7 @@ VALU_SIMDS = 256 * 4
 VALU_CLOCK_GHZ = 2.4
 VALU_CYCLES = {"b32": 2, "f64": 4, "trans64": 8}
 STRIPE_H = 16
+PIPE_REPS = 4   # single_frame.pipelined: passes over the single-frame views
 
 
 def parse():
@@ -117,6 +120,9 @@ def parse():
                          "views; 0 = every frame the same camera")
     ap.add_argument("--single-frames", type=int, default=16,
                     help="after the timed run: this many one-frame launches, timed the same way (single_frame record)")
+    ap.add_argument("--pipeline", type=int, default=3,
+                    help="one GPU: after the single-frame records, the same one-frame launches with this many in "
+                         "flight on streams of their own (single_frame.pipelined); <= 1 = off")
     ap.add_argument("--frame-budget-gb", type=float, default=8.0,
                     help="device memory for one stream's frame buffers; caps frames per launch at large sizes")
     ap.add_argument("--streams", type=int, default=0,
@@ -590,6 +596,24 @@ def main():
                            "natural (launches alternate streams)")
         single["natural_order"] = natural
         single["views"] = "consecutive camera-orbit views, one per launch"
+        # the same call shape with a.pipeline launches in flight (one stream each, round robin): a
+        # caller that keeps frames in flight lets launch i+1's waves fill launch i's drain, which
+        # serial one-frame launches pay in full (r05zv: 0.417 ms -> 0.349 / 0.338 ms per frame at
+        # 2 / 3 in flight).  The streams are not the cost maps' stream, so the order is natural
+        if n == 1 and S == 1 and a.pipeline > 1:
+            pst = [torch.cuda.Stream() for _ in range(a.pipeline)]
+            pbuf = [torch.empty((rows_max, W, 3), dtype=torch.float32, device="cuda") for _ in range(a.pipeline)]
+
+            def pipelined():
+                for li in range(PIPE_REPS * NS):
+                    gpu.launch(cams[li % NS], pbuf[li % a.pipeline].data_ptr(), stats=False,
+                               stream=pst[li % a.pipeline].cuda_stream)
+            pipelined()
+            el = timed_region(pipelined)
+            single["pipelined"] = {"launches_in_flight": a.pipeline, "frames": PIPE_REPS * NS,
+                                   "ms_per_frame": round(el / (PIPE_REPS * NS) * 1e3, 4),
+                                   "order": "natural (streams other than the cost maps' stream)",
+                                   "views": f"the {NS} views above, {PIPE_REPS} times"}
 
     # other device hierarchies over the same records (pixels and ray counts are identical for every
     # tree, tests/test_gpu_parity.py::test_device_tree_changes_no_pixel): the same run shape, timed the
@@ -672,7 +696,7 @@ def main():
         ms_per_step = elapsed / a.steps * 1e3
         mrays = rays_total / elapsed / 1e6
         if single is not None:
-            for rec in (single, single["natural_order"]):
+            for rec in (single, single["natural_order"]) + ((single["pipelined"],) if "pipelined" in single else ()):
                 rec["rays_per_frame"] = int(rays_frame0)
                 rec["value"] = round(rays_frame0 / (rec["ms_per_frame"] * 1e-3) / 1e6, 2)
                 rec["unit"] = "Mrays/s"
@@ -757,6 +781,7 @@ def main():
                 # frames the production kernel rendered in this process (counting launches, warm-up,
                 # timed run, single-frame run): the divisor tools/pmc_summary.py uses for per-frame bytes
                 "production_frames_rendered": (F + rem + NS + a.warmup + a.steps + (3 * NS if single else 0)
+                                               + (2 * PIPE_REPS * NS if single and "pipelined" in single else 0)
                                                if not a.adaptive else None),
                 "device_scene_MB": round(gpu.device_bytes / 1e6, 1),
                 **({"upload_options": upload_opts} if upload_opts else {}),

@@ -61,6 +61,9 @@ def test_bench_json_contract_and_saved_frame(tmp_path, frames):
     assert sf["frames"] == min(16, frames) and sf["ms_per_frame"] > 0 and sf["value"] > 0
     co = sf["natural_order"]
     assert co["frames"] == sf["frames"] and co["ms_per_frame"] > 0 and co["rays_per_frame"] == sf["rays_per_frame"]
+    pl = sf["pipelined"]   # the same one-frame launches, 3 in flight
+    assert pl["launches_in_flight"] == 3 and pl["frames"] == 4 * sf["frames"] and pl["ms_per_frame"] > 0
+    assert pl["rays_per_frame"] == sf["rays_per_frame"] and pl["value"] > 0
     ref, rays = expected_frames(320, 180, frames)
     assert np.array_equal(np.load(out), ref)
     assert d["config"]["rays_per_frame"] == rays
