@@ -405,12 +405,15 @@ def main():
     starts, ends, launch_frames = [], [], []
     gstarts, gends = [], []   # N > 1: HIP events around each launch's gather + re-interleave
 
+    warmed = set()   # streams that have carried a launch (a stream's first launch pays set-up)
+
     def launch(li, nf, timed, flags=0):
         """Launch li renders nf frames (steps); their stripes are then gathered to rank 0 (or, with
         the peer assembly, written there by the render itself and fenced).  A one-frame launch
         renders view cams[li % F] (the single-frame records: consecutive frames of the orbit)."""
         nonlocal image
         s = streams[li % S]
+        warmed.add(li % S)
         bs = [fbufs[li % S][f] for f in range(nf)]
         if assembly == "peer":
             outs = peer_frames().outs(li % S, nf)
@@ -497,12 +500,22 @@ def main():
             dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         return float(tmax[0])
 
+    stream_warm_frames = 0   # one-frame launches that only warmed a stream (counted below)
+
     def timed_run(warm):
         """warm-up frames, then the timed run of a.steps frames: (seconds (max over ranks), mean
         launch ms, mean gather ms); the per-launch event lists are refilled."""
+        nonlocal stream_warm_frames
         for lst in (starts, ends, launch_frames, gstarts, gends):
             lst.clear()
         run(warm, False)
+        # every stream the timed run uses has carried a launch before it: a stream's first launch
+        # pays its hardware queue's set-up (r05zv: two 10-frame launches on two streams, the second
+        # stream new, 10.1 ms against 8.0 ms of launch time)
+        for i in range(min(S, -(-a.steps // per_launch_of(assembly)))):
+            if i not in warmed:
+                launch(i, 1, False)
+                stream_warm_frames += 1
         el = timed_region(lambda: run(a.steps, True))
         k_ms = float(np.mean([s_.elapsed_time(e_) for s_, e_ in zip(starts, ends)]))
         g_ms = float(np.mean([s_.elapsed_time(e_) for s_, e_ in zip(gstarts, gends)])) if gstarts else 0.0
@@ -780,7 +793,8 @@ def main():
                 "upload_wall_s": round(upload_wall_s, 4),
                 # frames the production kernel rendered in this process (counting launches, warm-up,
                 # timed run, single-frame run): the divisor tools/pmc_summary.py uses for per-frame bytes
-                "production_frames_rendered": (F + rem + NS + a.warmup + a.steps + (3 * NS if single else 0)
+                "production_frames_rendered": (F + rem + NS + a.warmup + a.steps + stream_warm_frames
+                                               + (3 * NS if single else 0)
                                                + (2 * PIPE_REPS * NS if single and "pipelined" in single else 0)
                                                if not a.adaptive else None),
                 "device_scene_MB": round(gpu.device_bytes / 1e6, 1),
