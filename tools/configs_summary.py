@@ -29,6 +29,7 @@ def main(src, dst):
             "kernel_ms_per_frame": d.get("kernel_ms_per_frame"),
             "frames_per_launch": d["config"]["frames_per_launch"], "rays_per_frame": d["config"]["rays_per_frame"],
             "single_frame_ms": sf.get("ms_per_frame"),
+            "single_frame_pipelined_ms": (sf.get("pipelined") or {}).get("ms_per_frame"),
             "roofline_frac": (d.get("roofline") or {}).get("frac"),
             "bound": (d.get("roofline") or {}).get("bound"),
             "cpu_mrays_s": cb.get("value"), "cpu_threads": cb.get("cores"), "cpu_frame_s": cb.get("frame_s"),
