@@ -2683,6 +2683,14 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   const long long waves_needed = (P.n_tiles * 64 + 63) / 64;
   int bpc = sc->blocks_per_cu[v];
   if (sc->bpc_cap > 0) bpc = std::min(bpc, sc->bpc_cap);   // a smaller persistent grid (upload option)
+  // one-frame launches in flight on several streams (a caller pipelining the reference's call
+  // shape): while the previous launch, on another stream, still runs, this one takes half the
+  // block slots, so two launches are co-resident and each one's drain runs beside the other's work
+  // (3 in flight: 0.334 -> 0.325 ms per frame at half grids, r05zzb; multi-frame launches in
+  // flight lose with half grids, r05zzc, and keep the whole grid)
+  if (n_frames == 1 && sc->last_ctx >= 0 && sc->last_stream != st &&
+      hipEventQuery(sc->ctx[sc->last_ctx].ev1) == hipErrorNotReady)
+    bpc = std::max(1, bpc / 2);
   long long blocks = (long long)(sc->n_cu - sc->reserve_cus) * bpc;
   blocks = std::max<long long>(1, std::min<long long>(blocks, (waves_needed + kBlock / 64 - 1) / (kBlock / 64)));
   blocks = std::min<long long>(blocks, (long long)(sc->nslots / kBlock));
