@@ -2484,6 +2484,16 @@ int masked_stream(rt_scene* sc, hipStream_t caller, hipStream_t* out) {
 // (at most list_cap of them) of the full frame.
 // n_frames > 1 (rt_launch_frames): params p[0..n_frames) differ only in their camera vectors,
 // frame f is written to outs[f].
+// Has the work before event e finished?  hipErrorNotReady from the query is an answer, not a
+// failure; should a HIP runtime keep it as the last error, it is taken back out, so a caller's later
+// error check (torch's launch checks) does not report it (ROCm 7 on the MI355X box does not keep it:
+// tools/notready_probe.py, profiles/r05/r05zzh_notready.txt)
+static bool event_done(hipEvent_t e) {
+  const hipError_t q = hipEventQuery(e);
+  if (q == hipErrorNotReady && hipPeekAtLastError() == hipErrorNotReady) (void)hipGetLastError();
+  return q == hipSuccess;
+}
+
 int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* const* outs, rt_stats* stats,
                   void* stream, const uint32_t* list, const unsigned long long* count, long long list_cap,
                   double* sample_out = nullptr) {
@@ -2689,7 +2699,7 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   // (3 in flight: 0.334 -> 0.325 ms per frame at half grids, r05zzb; multi-frame launches in
   // flight lose with half grids, r05zzc, and keep the whole grid)
   if (n_frames == 1 && sc->last_ctx >= 0 && sc->last_stream != st &&
-      hipEventQuery(sc->ctx[sc->last_ctx].ev1) == hipErrorNotReady)
+      !event_done(sc->ctx[sc->last_ctx].ev1))
     bpc = std::max(1, bpc / 2);
   long long blocks = (long long)(sc->n_cu - sc->reserve_cus) * bpc;
   blocks = std::max<long long>(1, std::min<long long>(blocks, (waves_needed + kBlock / 64 - 1) / (kBlock / 64)));
@@ -2700,7 +2710,7 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   // the context's previous launch done (device side) and its staged copy consumed (host side); a
   // launch eight back has normally ended, and then no wait goes into the stream
   // (with the events below: one frame per call 0.4130 -> 0.4089 ms kernel, 0.4295 -> 0.4265 ms call; r05p)
-  if (C.used && hipEventQuery(C.ev1) != hipSuccess) {
+  if (C.used && !event_done(C.ev1)) {
     HIP_TRY(hipStreamWaitEvent(st, C.ev1, 0));
     HIP_TRY(hipEventSynchronize(C.ev1));
   }
