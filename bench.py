@@ -76,10 +76,12 @@ L1_PEAK_SOURCE = ("measured, not a datasheet figure (MI355X_MICROARCH.md gives n
                   "L1-resident dependent gather, 16 cycles of a CU's TD per 64-lane dwordx4 wave-instruction "
                   "touching <= 16 lines = 64 B/clk/CU (profiles/r05/l1_micro_r05.txt)")
 # roofline.bound vocabulary: the resource whose measured fraction of its peak is at least
-# BOUND_FRAC ("hbm": HBM bytes, "l1": vector-L1 data return, "valu": VALU issue); none of them ->
-# "latency" (each wave's dependent chain of fetches and ALU at 4 waves per SIMD)
+# BOUND_FRAC ("hbm": HBM bytes, "l1": vector-L1 data return, "valu": VALU issue); none of them, with
+# the HBM and VALU fractions both measured -> "latency" (each wave's dependent chain of fetches and
+# ALU at 4 waves per SIMD); none of them and one of those two not measured (no
+# committed PMC summary for the workload) -> "unmeasured"
 BOUND_FRAC = 0.8
-BOUND_VOCAB = ("hbm", "l1", "valu", "latency")
+BOUND_VOCAB = ("hbm", "l1", "valu", "latency", "unmeasured")
 # VALU issue (MI355X_MICROARCH.md, "Per-instruction cycle constants"): a SIMD-32 issues a 32-bit
 # wave64 VALU instruction in 2 cycles (4 cycles is what ONE wave alone sustains), an fp64 one in 4
 # (16 lanes per cycle: 78.6 TF fp64 = half the fp32 rate), a transcendental in 8 (the issue-cost
@@ -154,6 +156,12 @@ def parse():
     ap.add_argument("--assembly-ab", choices=["auto", "on", "off"], default="auto",
                     help="N > 1: after the timed run, time the same run with the other assembly and check that both "
                          "assemble bit-identical frames (multi_gpu.assembly_ab); auto = on at N > 1 without --adaptive")
+    ap.add_argument("--rank-shape", type=int, default=0, metavar="N",
+                    help="one process, one GPU: render exactly what rank 0 of an N-GPU run renders (its 16-row "
+                         "stripes of every frame, the N > 1 launch shape: frames per launch of the RCCL gather "
+                         "assembly, two launches in flight) with no collective, so rocprofv3 can profile the N-GPU "
+                         "rank shape on one GPU; the line's workload_key carries n_gpus = N, so an N-GPU run finds "
+                         "the PMC summary of this shape (roofline at N > 1).  value = this shard's rays/s")
     ap.add_argument("--launch-check", action="store_true",
                     help="start the ranks (--gpus N), join a gloo process group, check its size, print one JSON line "
                          "and exit before any GPU call (a dry run of the N-rank launch)")
@@ -238,6 +246,10 @@ def main():
     n = world
     if a.launch_check:
         return launch_check(a, n, rank)
+    if a.rank_shape and (n > 1 or a.rank_shape < 2 or a.adaptive):
+        raise SystemExit("bench.py: --rank-shape N (N >= 2) is a one-process run without --adaptive")
+    # the stripe partition and launch shape of this process: N > 1 ranks, or rank 0 of --rank-shape N
+    shape_n = a.rank_shape or n
     # rehearsal of the N-rank path on fewer GPUs (dev only): --dist-backend gloo stages the
     # collectives through host memory and RT_BENCH_DEVICE pins every rank to one device
     dev = int(os.environ.get("RT_BENCH_DEVICE", local))
@@ -264,12 +276,12 @@ def main():
     dev_build_s, dev_copy_s = gpu.upload_seconds
     params = host.render_params(a.width, a.height, a.spp)
     params.stripe_height = STRIPE_H
-    params.stripe_count = n
+    params.stripe_count = shape_n
     params.stripe_index = rank
     W = a.width
-    rows_max = shard_max_rows(a.height, STRIPE_H, n)
+    rows_max = shard_max_rows(a.height, STRIPE_H, shape_n)
     # librt_hip keeps 8 launch contexts per scene; the halo exchange of --adaptive is single-stream
-    S = 1 if a.adaptive else max(1, min(a.streams or (1 if n == 1 else 2), 8))
+    S = 1 if a.adaptive else max(1, min(a.streams or (1 if shape_n == 1 else 2), 8))
     # --adaptive on one GPU: F frames per launch for both passes (rt_launch_frames for the fp64
     # primary images, rt_launch_adaptive_frames for the supersampling of all F frames); on N > 1
     # one frame per launch (the halo exchange is per frame)
@@ -283,7 +295,7 @@ def main():
         """Frames per launch of the timed run.  N > 1 with the RCCL gather: at most half the steps,
         so the run has two launches and the gather of one can overlap the next launch; the peer
         assembly has nothing to overlap, so its frames go in launches of F (one drain per F)."""
-        if n > 1 and mode == "gather" and not a.frames and not a.adaptive:
+        if shape_n > 1 and mode == "gather" and not a.frames and not a.adaptive:
             return min(F, max(1, (a.steps + 1) // 2))
         return F
     # the animation path: frame f of every launch (the batched frames are distinct views)
@@ -380,8 +392,11 @@ def main():
     work_bytes_frame = (64 * tst.node_visits + 48 * tst.tri_tests + 64 * tst.closest_hits) / F
     fetch_bytes_frame = (128 * wst.node_visits + 80 * wst.tri_tests + 96 * wst.closest_hits) / F
 
-    gathers = [StripeGather(a.height, W, STRIPE_H, n, rank, device="cuda", frames=F, host_staged=host_staged)
-               for _ in range(S)]
+    if a.rank_shape:   # rank 0's stripes stay where they are rendered: no collective in this shape
+        gathers = [lambda b: b] * S
+    else:
+        gathers = [StripeGather(a.height, W, STRIPE_H, n, rank, device="cuda", frames=F, host_staged=host_staged)
+                   for _ in range(S)]
     image = None
     # N > 1 assembly by peer stores (--assembly peer): rank 0's whole frames, mapped by every rank;
     # the launches write global rows (RT_FLAG_GLOBAL_ROWS)
@@ -713,7 +728,10 @@ def main():
                 rec["rays_per_frame"] = int(rays_frame0)
                 rec["value"] = round(rays_frame0 / (rec["ms_per_frame"] * 1e-3) / 1e6, 2)
                 rec["unit"] = "Mrays/s"
-        pmc = pmc_per_frame(workload_key(a, n), frames_per_launch)
+        # (N > 1: the PMC summary of the rank shape -- rank 0's launches profiled on one GPU with
+        # --rank-shape N -- so the fractions are per GPU, of rank 0's kernel)
+        key = workload_key(a, shape_n)
+        pmc = pmc_per_frame(key, frames_per_launch)
         kernel_s = kernel_ms_avg * 1e-3
         roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": None,
                 "traffic": None}
@@ -747,8 +765,8 @@ def main():
                         "def": "128*wide_node_visits + 80*tri_tests + 96*closest_hits (production kernel's "
                                "4-wide diagnostic variant) / (64 B/clk x 256 CUs x 2.4 GHz)",
                         "peak_source": L1_PEAK_SOURCE},
-            "wave_cycles": pmc_wave_mix(workload_key(a, n), frames_per_launch),
-            "valu_roof": pmc_valu_roof(workload_key(a, n), frames_per_launch, kernel_s / frames_per_launch),
+            "wave_cycles": pmc_wave_mix(key, frames_per_launch),
+            "valu_roof": pmc_valu_roof(key, frames_per_launch, kernel_s / frames_per_launch),
         })
         roof["bound"], roof["bound_basis"] = binding_resource(roof)
         out = {
@@ -770,7 +788,7 @@ def main():
             "config": {
                 "workload": f"{a.scene}_proxy {a.width}x{a.height} spp={a.spp * a.spp} depth={params.max_depth} "
                             f"lights={params.n_lights}",
-                "workload_key": workload_key(a, n),
+                "workload_key": workload_key(a, shape_n),
                 "triangles": host.triangle_count,
                 "bvh": f"host: reference median split, depth {host.bvh_depth}; device: "
                        + {"sah": "binned-SAH hierarchy, 4-wide", "sbvh": "binned SAH with spatial splits, 4-wide",
@@ -778,7 +796,8 @@ def main():
                 "rays_per_frame": int(rays_total / a.steps),
                 "rays_breakdown_rank0_launch": {"primary": st.primary_rays, "shadow": st.shadow_rays,
                                                 "reflection": st.reflection_rays, "frames": F},
-                "parallelism": f"row-stripes x{n} (16-row interleave) + RCCL gather" if n > 1 else "single GPU",
+                "parallelism": (f"row-stripes x{n} (16-row interleave) + RCCL gather" if n > 1 else
+                                f"rank 0 of row-stripes x{shape_n}, alone on one GPU" if a.rank_shape else "single GPU"),
                 "frames_per_launch": frames_per_launch,
                 "animation": (f"camera orbit, {a.sweep} rad over each launch's {F} frames (distinct views)"
                               if F > 1 and a.sweep != 0.0 else "none (identical frames)"),
@@ -802,6 +821,11 @@ def main():
             },
             "single_frame": single,
             "multi_gpu": multi,
+            "rank_shape": ({"n_gpus": shape_n, "stripe_index": 0, "rows_per_frame": rows_local,
+                            "def": f"rank 0's share of a {shape_n}-GPU run (its {STRIPE_H}-row stripes of every "
+                                   "frame, the N > 1 launch shape) rendered alone on one GPU, no collective: the "
+                                   "shape whose rocprofv3 counters give the roofline of N > 1 lines; value = "
+                                   "this shard's rays/s, not a whole-job rate"} if a.rank_shape else None),
             "tree_records": tree_records,
             "roofline": roof,
             "cpu_baseline": None,
@@ -832,7 +856,8 @@ def binding_resource(roof):
     """(bound, basis) from the measured fractions in a roofline record: HBM (roof.frac), the
     vector-L1 data path (l1_roof.frac: useful fetch bytes / data-return peak) and VALU issue
     (valu_roof.frac).  The largest fraction names the bound when it reaches BOUND_FRAC; else no
-    throughput roof binds and the kernel is latency-bound (per-wave dependent chains, wave_cycles).
+    throughput roof binds and the kernel is latency-bound (per-wave dependent chains, wave_cycles) --
+    a claim that needs the HBM and VALU fractions measured: without either, "unmeasured".
     TD busy is not used: it counts cycles the TD holds requests waiting on L2."""
     fr = {"hbm": roof.get("frac"), "l1": (roof.get("l1_roof") or {}).get("frac"),
           "valu": (roof.get("valu_roof") or {}).get("frac")}
@@ -842,11 +867,14 @@ def binding_resource(roof):
     if wc:
         basis["wave_mem_wait_frac"] = wc.get("mem_wait_frac")
         basis["wave_issue_frac"] = wc.get("issue_frac")
-    basis["rule"] = f"largest measured fraction >= {BOUND_FRAC} names the roof, else latency"
+    basis["rule"] = (f"largest measured fraction >= {BOUND_FRAC} names the roof, else latency if the hbm and valu "
+                     "fractions are both measured, else unmeasured")
     if known:
         k, v = max(known.items(), key=lambda kv: kv[1])
         if v >= BOUND_FRAC:
             return k, basis
+    if fr["hbm"] is None or fr["valu"] is None:
+        return "unmeasured", basis
     return "latency", basis
 
 

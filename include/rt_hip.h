@@ -48,7 +48,10 @@ extern "C" {
 
 /* Lights held inline in rt_render_params (and staged in LDS by the kernel).  Scenes with
  * more lights pass them through rt_render_params.lights_ext (any count up to
- * RT_LIGHTS_LIMIT); the reference shades any nLights (mytracer_gpu.cu:632). */
+ * RT_LIGHTS_LIMIT); the reference shades any nLights (mytracer_gpu.cu:632).  Every launch copies
+ * its light table with its control block (as the reference's copyLights per call,
+ * mytracer.cpp:105-118), so lights may change from call to call, on any stream, without a
+ * device synchronisation. */
 #define RT_MAX_LIGHTS 16
 #define RT_LIGHTS_LIMIT (1 << 20)
 
@@ -122,7 +125,8 @@ enum {
                                   are written at their global positions (row y at y * width * 3), not packed.
                                   With a peer GPU's frame buffer (rt_ipc_open) every rank writes its stripes
                                   straight into the assembled frame over xGMI; each wave's stores are released
-                                  at system scope before it exits.  Not for the adaptive pass */
+                                  at system scope before it exits.  Not for the adaptive pass nor
+                                  rt_render_to_host (RT_ERR_INVALID) */
 };
 
 /* One render call.  Rows are rendered as interleaved stripes:
@@ -368,8 +372,17 @@ int rt_ipc_open(const unsigned char* handle, unsigned long long offset, int devi
 int rt_ipc_close(void* d_ptr, unsigned long long offset);
 
 /* Milliseconds of the last launch on this scene, measured with hipEvents
- * recorded around the kernel on its stream (valid after the stream syncs). */
+ * recorded around the kernel on its stream (waits for it).  Returns RT_ERR_HIP when a launch on
+ * the scene tripped the kernel watchdog (rt_scene_status). */
 int rt_last_kernel_ms(rt_scene* scene, float* ms);
+
+/* RT_OK, or RT_ERR_HIP once any finished launch on this scene tripped a kernel watchdog (a
+ * traversal loop that ran past its iteration bound: a cyclic or corrupt hierarchy, or a kernel
+ * bug).  The kernel mirrors the flag into page-locked host memory, so launches without stats
+ * report it too: from then on every launch on the scene, rt_last_kernel_ms and this call return
+ * RT_ERR_HIP (sticky; the scene's results are void -- free it and upload again).  Replaces the
+ * reference's CHECK-and-continue (common/common.h:6-15).  Does not synchronise. */
+int rt_scene_status(const rt_scene* scene);
 
 /* Diagnostics: raw device counter words of the last launch (synchronises the
  * device).  Words [8,16) = rt_stats order (from node_visits on: STATS flags only;
@@ -394,6 +407,18 @@ long long rt_debug_wave_log(rt_scene* scene, unsigned long long* out, long long 
 /* Diagnostics: persistent-grid blocks per CU of kernel variant 0 (production), 1 (4-wide
  * STATS), 2 (2-wide canonical STATS) or 3 (timeline), as the launches use it. */
 int rt_debug_blocks_per_cu(rt_scene* scene, int variant);
+
+/* Diagnostics: the persistent grid (blocks) the last launch on the scene used, and the grid a
+ * launch of that shape gets when the device is otherwise idle.  They differ for a one-frame launch
+ * issued while the scene's previous launch, on another stream, was still running: it takes half
+ * the block slots, so the two overlap (pixels and counts do not depend on it).  Either pointer may
+ * be NULL. */
+int rt_debug_last_grid(rt_scene* scene, long long* blocks, long long* full_blocks);
+
+/* Test hook: replaces the scene's first 4-wide node by a cycle (its one child is itself, with a
+ * box that holds every ray), so every production traversal that enters the hierarchy loops until
+ * the kernel watchdog ends it.  Synchronises the device.  The scene is unusable afterwards. */
+int rt_debug_corrupt_hierarchy(rt_scene* scene);
 
 /* Diagnostics: per-round timeline of the last launch with RT_FLAG_TIMELINE: for wave w of the
  * persistent grid and its r-th traversal round (r < 256), words [8(256w + r), +8) = {round start,

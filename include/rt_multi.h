@@ -41,9 +41,23 @@ int rt_multi_device_count(const rt_multi* m);
  * launch writes its stripes straight into the output frames on devices[0] over xGMI
  * (RT_FLAG_GLOBAL_ROWS), with no copy and no re-interleave.  Setting RT_MULTI_PEER checks and
  * enables peer access from every device to devices[0]; it fails (RT_ERR_UNSUPPORTED, the
- * driver unchanged) when a device cannot access it. */
+ * driver unchanged) when a device cannot access it.  Guard: before its first peer render the
+ * driver renders a corner window of the caller's first frame (at most 128 x 2n stripes, every GPU
+ * rendering rows of it) once by the gather and once by peer stores and keeps the peer assembly
+ * only if the two are bit-identical; otherwise it gathers from then on (rt_multi_assembly tells
+ * which is in use).  Setting RT_MULTI_PEER again re-arms the check.  The calling thread's current
+ * device is left as it was by every rt_multi call. */
 enum { RT_MULTI_GATHER = 0, RT_MULTI_PEER = 1 };
 int rt_multi_set_assembly(rt_multi* m, int assembly);
+
+/* The frame assembly in use: RT_MULTI_GATHER or RT_MULTI_PEER (RT_MULTI_GATHER after the peer guard
+ * refused peer stores). */
+int rt_multi_assembly(const rt_multi* m);
+
+/* Test hook: what = RT_MULTI_DEBUG_PEER_MISMATCH corrupts one word of the peer guard's frame, so
+ * the guard must refuse the peer assembly; 0 = off. */
+enum { RT_MULTI_DEBUG_PEER_MISMATCH = 1 };
+int rt_multi_debug_inject(rt_multi* m, int what);
 
 /* Renders one whole frame (rt_multi_render_frames with one frame; p->row_begin / row_end / stripe_* are ignored: every row is
  * rendered, sharded as above with the given stripe_height >= 1) into d_out, a DEVICE

@@ -35,6 +35,18 @@ int fail(int code, const std::string& msg) {
     if (r_ != ncclSuccess) return fail(RT_ERR_HIP, std::string(#call) + ": " + ncclGetErrorString(r_)); \
   } while (0)
 
+// Restores the calling thread's current device when an entry point returns (every return path):
+// the driver switches devices internally, the caller's own device stays current.
+struct DeviceRestore {
+  int dev = -1;
+  DeviceRestore() {
+    if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+  }
+  ~DeviceRestore() {
+    if (dev >= 0) (void)hipSetDevice(dev);
+  }
+};
+
 // Shard g renders the rows (y / sh) % n == g packed in increasing y: global row y sits in
 // shard (y / sh) % n at local row (y / sh / n) * sh + y % sh.  Shared by the device kernel
 // and the host restatement.
@@ -109,6 +121,11 @@ struct rt_multi {
   size_t sbuf_bytes = 0;       // bytes of every slot's per-device stripe buffer
   void* d_host_stage = nullptr;   // rt_multi_render_to_host: the assembled frame on devices[0], kept
   size_t host_stage_bytes = 0;
+  // RT_MULTI_PEER guard: before its first peer render the driver renders a corner window of the
+  // caller's first frame both ways and keeps peer only if the two frames are bit-identical
+  bool peer_checked = false;
+  bool peer_refused = false;
+  int debug = 0;                  // rt_multi_debug_inject
 };
 
 extern "C" {
@@ -138,6 +155,7 @@ int rt_multi_interleave_frames_host(const void* gathered, void* const* outs, int
 
 void rt_multi_free(rt_multi* m) {
   if (!m) return;
+  DeviceRestore keep;
   for (int g = 0; g < (int)m->devices.size(); ++g) {
     (void)hipSetDevice(m->devices[g]);
     (void)hipDeviceSynchronize();
@@ -165,6 +183,7 @@ int rt_multi_create(const rt_scene_soa* soa, const rt_bvh_soa* bvh, const int* d
                     const rt_upload_options* opt, rt_multi** out) {
   if (!out || !devices || n_devices < 1) return fail(RT_ERR_INVALID, "rt_multi_create: bad argument");
   *out = nullptr;
+  DeviceRestore keep;
   for (int a = 0; a < n_devices; ++a)
     for (int b = a + 1; b < n_devices; ++b)
       if (devices[a] == devices[b]) return fail(RT_ERR_INVALID, "rt_multi_create: device ids must be distinct");
@@ -218,6 +237,7 @@ int rt_multi_device_count(const rt_multi* m) { return m ? m->n : 0; }
 int rt_multi_set_assembly(rt_multi* m, int assembly) {
   if (!m || (assembly != RT_MULTI_GATHER && assembly != RT_MULTI_PEER))
     return fail(RT_ERR_INVALID, "rt_multi_set_assembly: bad argument");
+  DeviceRestore keep;
   if (assembly == RT_MULTI_PEER)
     for (int g = 1; g < m->n; ++g) {   // kernels on devices[g] store into devices[0]'s frames
       int can = 0;
@@ -232,6 +252,19 @@ int rt_multi_set_assembly(rt_multi* m, int assembly) {
       (void)hipGetLastError();
     }
   m->assembly = assembly;
+  m->peer_checked = false;   // a peer assembly is verified again before its first render
+  m->peer_refused = false;
+  return RT_OK;
+}
+
+int rt_multi_assembly(const rt_multi* m) {
+  if (!m) return fail(RT_ERR_INVALID, "rt_multi_assembly: null driver");
+  return m->assembly;
+}
+
+int rt_multi_debug_inject(rt_multi* m, int what) {
+  if (!m || what < 0) return fail(RT_ERR_INVALID, "rt_multi_debug_inject: bad argument");
+  m->debug = what;
   return RT_OK;
 }
 
@@ -285,26 +318,12 @@ static int batch_cap(int n, size_t shard_bytes) {
   return (int)std::max<size_t>(1, std::min<size_t>(RT_MAX_FRAMES, budget / per_frame));
 }
 
-int rt_multi_render_frames(rt_multi* m, const rt_render_params* p, int n_frames, int stripe_height,
-                           void* const* d_outs, rt_stats* stats, double* ms) {
-  if (!m || !p || !d_outs || stripe_height < 1 || n_frames < 1)
-    return fail(RT_ERR_INVALID, "rt_multi_render_frames: bad argument");
-  if (p->out_format != RT_OUT_RGB_F32 && p->out_format != RT_OUT_RGB_F64)
-    return fail(RT_ERR_INVALID, "rt_multi_render_frames: bad out_format");
+namespace {
+// RT_MULTI_GATHER: batches of frames, every GPU's stripes of a batch in one launch, one grouped
+// ncclGather of the batch to devices[0] and one re-interleave kernel there; two batches in flight.
+int render_frames_gather(rt_multi* m, const rt_render_params* p, int n_frames, int stripe_height,
+                         void* const* d_outs, rt_stats* stats) {
   const int n = m->n, W = p->camera.width, H = p->camera.height;
-  if (W <= 0 || H <= 0) return fail(RT_ERR_INVALID, "rt_multi_render_frames: bad image size");
-  for (int f = 0; f < n_frames; ++f) {
-    if (!d_outs[f]) return fail(RT_ERR_INVALID, "rt_multi_render_frames: null output buffer");
-    if (p[f].camera.width != W || p[f].camera.height != H || p[f].out_format != p->out_format)
-      return fail(RT_ERR_INVALID, "rt_multi_render_frames: frames must share size and format");
-  }
-  if (m->assembly == RT_MULTI_PEER) {
-    if (stats) std::memset(stats, 0, sizeof *stats);
-    const auto t0 = std::chrono::steady_clock::now();
-    const int rc = render_frames_peer(m, p, n_frames, stripe_height, d_outs, stats);
-    if (ms) *ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    return rc;
-  }
   const int elem = p->out_format == RT_OUT_RGB_F64 ? 8 : 4;
   const int mr = max_rows_of(H, stripe_height, n);
   const size_t row_bytes = (size_t)W * 3 * elem;
@@ -331,8 +350,6 @@ int rt_multi_render_frames(rt_multi* m, const rt_render_params* p, int n_frames,
     }
     m->sbuf_bytes = need;
   }
-  if (stats) std::memset(stats, 0, sizeof *stats);
-  const auto t0 = std::chrono::steady_clock::now();
   std::vector<rt_render_params> q((size_t)per);
   std::vector<void*> outs((size_t)per);
   for (int b = 0, f0 = 0; f0 < n_frames; ++b, f0 += per) {
@@ -351,6 +368,7 @@ int rt_multi_render_frames(rt_multi* m, const rt_render_params* p, int n_frames,
         q[f].stripe_height = stripe_height;
         q[f].stripe_count = n;
         q[f].stripe_index = g;
+        q[f].flags &= ~RT_FLAG_GLOBAL_ROWS;   // the stripe buffers hold packed shard rows
         outs[f] = static_cast<unsigned char*>(S.sbuf[g]) + (size_t)f * shard_bytes;
       }
       rt_stats st;
@@ -390,9 +408,84 @@ int rt_multi_render_frames(rt_multi* m, const rt_render_params* p, int n_frames,
       HIP_TRY(hipStreamSynchronize(S.streams[g]));
     }
   for (Slot& S : m->slot) S.busy = false;
-  const double t = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  if (ms) *ms = t;
   return RT_OK;
+}
+
+// The RT_MULTI_PEER guard.  Peer frames are correct only if every GPU's image stores, written over
+// xGMI into devices[0]'s memory, are there once the GPU's launch has ended (each wave's system-scope
+// release before it exits; devices[0] reads them after the launches ended).  Before
+// its first peer render the driver checks that on this node: a corner window of the caller's first
+// frame (the same camera vectors, at most 128 x 2n stripes: every GPU renders rows of it) rendered
+// by the gather and by peer stores into two buffers on devices[0], compared bit for bit; *same =
+// whether they agree.
+int verify_peer(rt_multi* m, const rt_render_params* p, int stripe_height, bool* same) {
+  rt_render_params q = *p;
+  q.camera.width = std::min(p->camera.width, 128);
+  q.camera.height = std::min(p->camera.height, 2 * m->n * stripe_height);
+  const size_t bytes = (size_t)q.camera.width * q.camera.height * 3 * (p->out_format == RT_OUT_RGB_F64 ? 8 : 4);
+  HIP_TRY(hipSetDevice(m->devices[0]));
+  void* a = nullptr;
+  void* b = nullptr;
+  HIP_TRY(hipMalloc(&a, bytes));
+  if (hipMalloc(&b, bytes) != hipSuccess) {
+    (void)hipFree(a);
+    return fail(RT_ERR_HIP, "rt_multi peer check: hipMalloc failed");
+  }
+  std::vector<unsigned char> ha(bytes), hb(bytes);
+  int rc = RT_OK;
+  // different fills: a pixel left unwritten by either assembly shows as a difference
+  if (hipMemset(a, 0x00, bytes) != hipSuccess || hipMemset(b, 0xff, bytes) != hipSuccess)
+    rc = fail(RT_ERR_HIP, "rt_multi peer check: hipMemset failed");
+  if (rc == RT_OK) rc = render_frames_gather(m, &q, 1, stripe_height, &a, nullptr);
+  if (rc == RT_OK) rc = render_frames_peer(m, &q, 1, stripe_height, &b, nullptr);
+  if (rc == RT_OK && (m->debug & RT_MULTI_DEBUG_PEER_MISMATCH)) {   // test hook: one corrupted word
+    (void)hipSetDevice(m->devices[0]);
+    if (hipMemset(b, 0x7f, 4) != hipSuccess) rc = fail(RT_ERR_HIP, "rt_multi peer check: hipMemset failed");
+  }
+  if (rc == RT_OK) {
+    (void)hipSetDevice(m->devices[0]);
+    if (hipMemcpy(ha.data(), a, bytes, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(hb.data(), b, bytes, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = fail(RT_ERR_HIP, "rt_multi peer check: copy failed");
+  }
+  (void)hipSetDevice(m->devices[0]);
+  (void)hipFree(a);
+  (void)hipFree(b);
+  if (rc == RT_OK) *same = std::memcmp(ha.data(), hb.data(), bytes) == 0;
+  return rc;
+}
+}  // namespace
+
+int rt_multi_render_frames(rt_multi* m, const rt_render_params* p, int n_frames, int stripe_height,
+                           void* const* d_outs, rt_stats* stats, double* ms) {
+  if (!m || !p || !d_outs || stripe_height < 1 || n_frames < 1)
+    return fail(RT_ERR_INVALID, "rt_multi_render_frames: bad argument");
+  if (p->out_format != RT_OUT_RGB_F32 && p->out_format != RT_OUT_RGB_F64)
+    return fail(RT_ERR_INVALID, "rt_multi_render_frames: bad out_format");
+  const int W = p->camera.width, H = p->camera.height;
+  if (W <= 0 || H <= 0) return fail(RT_ERR_INVALID, "rt_multi_render_frames: bad image size");
+  for (int f = 0; f < n_frames; ++f) {
+    if (!d_outs[f]) return fail(RT_ERR_INVALID, "rt_multi_render_frames: null output buffer");
+    if (p[f].camera.width != W || p[f].camera.height != H || p[f].out_format != p->out_format)
+      return fail(RT_ERR_INVALID, "rt_multi_render_frames: frames must share size and format");
+  }
+  DeviceRestore keep;
+  if (m->assembly == RT_MULTI_PEER && !m->peer_checked) {   // the peer guard (untimed, once)
+    bool same = false;
+    const int rc = verify_peer(m, p, stripe_height, &same);
+    if (rc != RT_OK) return rc;
+    m->peer_checked = true;
+    if (!same) {   // refused: this driver gathers from now on (rt_multi_assembly reports it)
+      m->assembly = RT_MULTI_GATHER;
+      m->peer_refused = true;
+    }
+  }
+  if (stats) std::memset(stats, 0, sizeof *stats);
+  const auto t0 = std::chrono::steady_clock::now();
+  const int rc = m->assembly == RT_MULTI_PEER ? render_frames_peer(m, p, n_frames, stripe_height, d_outs, stats)
+                                              : render_frames_gather(m, p, n_frames, stripe_height, d_outs, stats);
+  if (ms) *ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return rc;
 }
 
 int rt_multi_render(rt_multi* m, const rt_render_params* p, int stripe_height, void* d_out, rt_stats* stats,
@@ -404,6 +497,7 @@ int rt_multi_render(rt_multi* m, const rt_render_params* p, int stripe_height, v
 int rt_multi_render_to_host(rt_multi* m, const rt_render_params* p, int stripe_height, void* host_out,
                             rt_stats* stats, double* ms) {
   if (!m || !p || !host_out) return fail(RT_ERR_INVALID, "rt_multi_render_to_host: bad argument");
+  DeviceRestore keep;
   const size_t bytes = (size_t)p->camera.width * p->camera.height * 3 * (p->out_format == RT_OUT_RGB_F64 ? 8 : 4);
   HIP_TRY(hipSetDevice(m->devices[0]));
   if (m->host_stage_bytes < bytes) {   // the frame's device buffer, kept between calls (grown as needed)

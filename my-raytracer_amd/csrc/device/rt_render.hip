@@ -171,6 +171,15 @@ enum : int {
 // the host reports as an error.
 constexpr unsigned kGuardIters = 1u << 24;
 constexpr unsigned kTravGuard = 1u << 24;
+// A watchdog fired: the launch's counter word (stats launches) and the scene's host-mapped word,
+// written with a vector store and released at system scope, so the host sees it after launches
+// without stats too (rt_scene_status).  One lane of the wave calls it.
+__device__ __forceinline__ void trip_watchdog(unsigned long long* ctr, unsigned int* host_word) {
+  atomicOr(&ctr[CD_GUARD], 1ull);
+  __builtin_nontemporal_store(1u, host_word);
+  __threadfence_system();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
 constexpr int kTlCap = 256;   // TL variant: traversal rounds recorded per wave
 constexpr int kTlWords = 8;   // ... and words per round
 
@@ -236,7 +245,8 @@ struct KParams {
   uint32_t* spill;      // [stack_words][nslots] traversal-stack entries below the LDS ring
   unsigned long long* wavelog;  // STATS: per wave {start, last refill, end, pixels} (s_memrealtime)
   unsigned long long* tl;       // TL: per wave and traversal round {start, end, lanes, iterations}
-  const double* lights; // [n_lights][6] position xyz, colour rgb
+  const double* lights; // [n_lights][6] position xyz, colour rgb (this launch's control block)
+  unsigned int* guard_host;   // the scene's watchdog word in page-locked host memory (trip_watchdog)
   size_t nslots;
   int n_gnodes;
   int out_fmt;
@@ -818,7 +828,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
   unsigned guard = 0;
   for (;;) {
     if (++guard > kGuardIters) {   // watchdog: end the wave instead of spinning, flag the launch
-      if (lane == 0) atomicOr(&P.ctr[CD_GUARD], 1ull);
+      if (lane == 0) trip_watchdog(P.ctr, P.guard_host);
       break;
     }
     if (STATS) { d_outer++; t_stamp = stamp(); }
@@ -1065,8 +1075,12 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
       // only inside that loop, so it stays wave-uniform (an SGPR: the check costs SALU only).
       // A loop that runs past kTravGuard iterations abandons the ray (results void) and flags
       // the launch.  (Cost: 0.3 % for the node loop, A/B.)
+      // (the wave then ends, below: a corrupt hierarchy costs each wave one guard's worth of
+      // iterations, not one per ray)
+      bool tripped = false;
       auto guard_trip = [&]() {
-        if (lane == __ffsll((long long)wballot(1)) - 1) atomicOr(&P.ctr[CD_GUARD], 1ull);
+        if (lane == __ffsll((long long)wballot(1)) - 1) trip_watchdog(P.ctr, P.guard_host);
+        tripped = true;
       };
       // tests the triangles of leaf `lref` in record order; true = any-hit ray occluded
       auto test_leaf = [&](uint32_t lref) -> bool {
@@ -1335,6 +1349,9 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
         }
       }
       thit = tlim;
+      // a watchdog fired in this traversal: the persistent loop's check ends the wave next time
+      // (wave-uniform here, so the loop counter stays scalar)
+      if (wballot(tripped) != 0ull) guard = kGuardIters;
     }
     asm volatile("" ::: "memory");
     if (STATS) { const unsigned long long t = stamp(); d_trav += t - t_stamp; t_stamp = t; }
@@ -1795,7 +1812,12 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
   }
   // RT_FLAG_GLOBAL_ROWS into a peer GPU's frame: this wave's image stores are written back to
   // memory before it exits (system-scope release), so they are there when the launch ends
-  if (P.out_global) __threadfence_system();
+  // (the explicit wait: ROCm 7.2 may drop the fence's own vmcnt wait after its L2 write-back when it
+  // believes the wave's counter empty, MI355X_MICROARCH.md "Compiler hazard")
+  if (P.out_global) {
+    __threadfence_system();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   // ---------------- counters: one atomic per wave and counter ----------------
   const unsigned long long s0 = wave_sum(c_primary), s1 = wave_sum(c_shadow), s2 = wave_sum(c_refl);
   unsigned long long s3 = 0, s4 = 0, s5 = 0;
@@ -2072,9 +2094,13 @@ int top_nodes_for(int stack_words, int ring, int n_gnodes4) {
 // reused only after its previous launch completed (stream wait on `done`).
 constexpr int kContexts = 8;
 struct LaunchCtx {
-  unsigned long long* d_ctr = nullptr;       // [kCtrWords] work heads, stats, diagnostics, then
-                                             // FrameDesc[kMaxFrames] (one H2D copy per launch)
+  unsigned long long* d_ctr = nullptr;       // control block: [kCtrWords] work heads, stats, diagnostics,
+                                             // then FrameDesc[n_frames], then the light table
+                                             // [n_lights][6] (one H2D copy per launch)
   unsigned char* h_ctl = nullptr;            // pinned staging of the same bytes
+  size_t ctl_cap = 0;                        // bytes of d_ctr / h_ctl (grown for > RT_MAX_LIGHTS lights)
+  long long blocks = 0;                      // persistent grid of the last launch (rt_debug_last_grid)
+  long long full_blocks = 0;                 // ... and the grid that launch shape gets on an idle device
   double* d_pstate = nullptr;                // path state, nslots x kRegions x 32 B
   uint32_t* d_spill = nullptr;               // [stack_words][nslots] (only when stack_words > kShortStack)
   unsigned long long* d_wavelog = nullptr;   // [nslots / 64][4]
@@ -2108,9 +2134,11 @@ struct rt_scene {
   int last_ctx = -1;            // context of the most recent launch
   hipStream_t last_stream = nullptr;   // ... and its stream
   size_t nslots = 0;
-  double* d_lights = nullptr;   // [light_cap][6] position xyz, colour rgb
-  int light_cap = 0;            // lights d_lights can hold
-  std::vector<double> cached_light_data;   // the table currently in d_lights
+  // kernel watchdog (CD_GUARD), mirrored by the kernel into page-locked host memory, so a launch
+  // without stats reports it too: the next launch on the scene, rt_last_kernel_ms and
+  // rt_scene_status return RT_ERR_HIP once it is set (sticky: the scene's results are void)
+  unsigned int* h_guard = nullptr;   // host view
+  unsigned int* d_guard = nullptr;   // the same word as the kernel addresses it
   double delta = 0.0;
   double root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};
   long long bytes = 0;
@@ -2279,18 +2307,20 @@ int upload_image(const SceneImage& I, const rt_upload_options& opt, int device, 
     max_blocks = std::max(max_blocks, nb);
   }
   sc->nslots = (size_t)sc->n_cu * max_blocks * kBlock;
-  if (hipMalloc(reinterpret_cast<void**>(&sc->d_lights), RT_MAX_LIGHTS * 6 * sizeof(double)) != hipSuccess) {
+  // the watchdog word: page-locked, mapped into the device's address space
+  if (hipHostMalloc(reinterpret_cast<void**>(&sc->h_guard), 64, hipHostMallocMapped) != hipSuccess ||
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&sc->d_guard), sc->h_guard, 0) != hipSuccess) {
     rt_scene_free(sc);
-    return fail(RT_ERR_HIP, "hipMalloc of lights failed");
+    return fail(RT_ERR_HIP, "allocation of the watchdog word failed");
   }
-  sc->light_cap = RT_MAX_LIGHTS;
-  sc->bytes += (long long)(RT_MAX_LIGHTS * 6 * sizeof(double));
+  *reinterpret_cast<volatile unsigned int*>(sc->h_guard) = 0u;
   for (LaunchCtx& c : sc->ctx) {
     const size_t pb = sc->nslots * kRegions * kLaneRec;
     const size_t wb = sc->nslots / 64 * 4 * sizeof(unsigned long long);
     const size_t sb = sc->stack_words > kShortStack ? sc->nslots * (size_t)sc->stack_words * sizeof(uint32_t) : 0;
-    if (hipMalloc(reinterpret_cast<void**>(&c.d_ctr), kCtlBytes) != hipSuccess ||
-        hipHostMalloc(reinterpret_cast<void**>(&c.h_ctl), kCtlBytes, hipHostMallocDefault) != hipSuccess ||
+    c.ctl_cap = kCtlBytes + RT_MAX_LIGHTS * 6 * sizeof(double);
+    if (hipMalloc(reinterpret_cast<void**>(&c.d_ctr), c.ctl_cap) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void**>(&c.h_ctl), c.ctl_cap, hipHostMallocDefault) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&c.d_pstate), pb) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&c.d_wavelog), wb) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&c.d_wctr), wb) != hipSuccess ||
@@ -2300,7 +2330,7 @@ int upload_image(const SceneImage& I, const rt_upload_options& opt, int device, 
       rt_scene_free(sc);
       return fail(RT_ERR_HIP, "allocation of launch contexts failed");
     }
-    sc->bytes += (long long)(kCtlBytes + pb + 2 * wb + sb);
+    sc->bytes += (long long)(c.ctl_cap + pb + 2 * wb + sb);
   }
   *out = sc;
   return RT_OK;
@@ -2494,6 +2524,16 @@ static bool event_done(hipEvent_t e) {
   return q == hipSuccess;
 }
 
+// Has a launch on this scene tripped a kernel watchdog (the CHECK-and-continue the reference has,
+// common/common.h:6-15, made an error)?  The kernel writes the flag into page-locked host memory
+// at system scope, so this sees launches that ended without stats, whatever their stream.
+const char* const kGuardMsg =
+    "a launch on this scene tripped the kernel watchdog (cyclic or corrupt hierarchy, or a kernel bug): "
+    "its pixels and every later result of this scene are void";
+static bool guard_tripped(const rt_scene* sc) {
+  return sc->h_guard && *reinterpret_cast<const volatile unsigned int*>(sc->h_guard) != 0u;
+}
+
 int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* const* outs, rt_stats* stats,
                   void* stream, const uint32_t* list, const unsigned long long* count, long long list_cap,
                   double* sample_out = nullptr) {
@@ -2524,6 +2564,7 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   const int rows = rt_rows_in_shard(p);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   HIP_TRY(hipSetDevice(sc->device));
+  if (guard_tripped(sc)) return fail(RT_ERR_HIP, kGuardMsg);
 
   KParams P;
   std::memset(&P, 0, sizeof P);
@@ -2544,6 +2585,29 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
     HIP_TRY(hipStreamWaitEvent(ks, C.ev_in, 0));
     st = ks;
   }
+  // the context's previous launch done (device side) and its staged copy consumed (host side); a
+  // launch eight back has normally ended, and then no wait goes into the stream
+  // (with the events below: one frame per call 0.4130 -> 0.4089 ms kernel, 0.4295 -> 0.4265 ms call; r05p)
+  if (C.used && !event_done(C.ev1)) {
+    HIP_TRY(hipStreamWaitEvent(st, C.ev1, 0));
+    HIP_TRY(hipEventSynchronize(C.ev1));
+  }
+  // control block of this launch: counters, frame table, light table (grown for a larger light
+  // table; the context is idle here, so its old buffers can go)
+  const size_t lights_at = kCtrBytes + (size_t)n_frames * sizeof(FrameDesc);
+  const size_t ctl_bytes = lights_at + (size_t)p->n_lights * 6 * sizeof(double);
+  if (ctl_bytes > C.ctl_cap) {
+    HIP_TRY(hipFree(C.d_ctr));
+    C.d_ctr = nullptr;
+    HIP_TRY(hipHostFree(C.h_ctl));
+    C.h_ctl = nullptr;
+    sc->bytes -= (long long)C.ctl_cap;
+    C.ctl_cap = 0;
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&C.d_ctr), ctl_bytes));
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&C.h_ctl), ctl_bytes, hipHostMallocDefault));
+    C.ctl_cap = ctl_bytes;
+    sc->bytes += (long long)ctl_bytes;
+  }
   P.ctr = C.d_ctr;
   P.heads = reinterpret_cast<unsigned long long*>(reinterpret_cast<unsigned char*>(C.d_ctr) + kHeadsOff);
   P.wctr = C.d_wctr;
@@ -2559,28 +2623,11 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   P.H = p->camera.height;
   P.n_lights = p->n_lights;
   P.max_depth = p->max_depth;
-  {  // lights live in device memory; re-uploaded (device-synchronising) only when they change
-    std::vector<double> ld(6 * (size_t)p->n_lights);
-    for (int i = 0; i < p->n_lights; ++i) {
-      const rt_light* L = rt_params_light(p, i);
-      for (int k = 0; k < 3; ++k) { ld[6 * i + k] = L->position[k]; ld[6 * i + 3 + k] = L->color[k]; }
-    }
-    if (ld != sc->cached_light_data) {
-      HIP_TRY(hipDeviceSynchronize());   // launches in flight may still read the old table
-      if (p->n_lights > sc->light_cap) {
-        HIP_TRY(hipFree(sc->d_lights));
-        sc->d_lights = nullptr;
-        sc->bytes -= (long long)(sc->light_cap * 6 * sizeof(double));
-        sc->light_cap = 0;
-        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&sc->d_lights), ld.size() * sizeof(double)));
-        sc->light_cap = p->n_lights;
-        sc->bytes += (long long)(ld.size() * sizeof(double));
-      }
-      if (!ld.empty()) HIP_TRY(hipMemcpy(sc->d_lights, ld.data(), ld.size() * sizeof(double), hipMemcpyHostToDevice));
-      sc->cached_light_data = std::move(ld);
-    }
-  }
-  P.lights = sc->d_lights;
+  // lights: in this launch's control block, staged with its counters and frame table (the
+  // reference copies them on every call too, mytracer.cpp:105-118); no device-wide synchronisation,
+  // so launches on other streams with other lights run on
+  P.lights = reinterpret_cast<const double*>(reinterpret_cast<unsigned char*>(C.d_ctr) + lights_at);
+  P.guard_host = sc->d_guard;
   P.pstate = C.d_pstate;
   P.spill = C.d_spill;
   P.wavelog = C.d_wavelog;
@@ -2693,28 +2740,27 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   const long long waves_needed = (P.n_tiles * 64 + 63) / 64;
   int bpc = sc->blocks_per_cu[v];
   if (sc->bpc_cap > 0) bpc = std::min(bpc, sc->bpc_cap);   // a smaller persistent grid (upload option)
+  auto grid_of = [&](int bpc_) {
+    long long b = (long long)(sc->n_cu - sc->reserve_cus) * bpc_;
+    b = std::max<long long>(1, std::min<long long>(b, (waves_needed + kBlock / 64 - 1) / (kBlock / 64)));
+    b = std::min<long long>(b, (long long)(sc->nslots / kBlock));
+    if (sc->grid_spare > 0)   // leave block slots to concurrent kernels (upload option)
+      b = std::max<long long>(1, b - sc->grid_spare);
+    return b;
+  };
+  const long long full_blocks = grid_of(bpc);
   // one-frame launches in flight on several streams (a caller pipelining the reference's call
   // shape): while the previous launch, on another stream, still runs, this one takes half the
   // block slots, so two launches are co-resident and each one's drain runs beside the other's work
   // (3 in flight: 0.334 -> 0.325 ms per frame at half grids, r05zzb; multi-frame launches in
-  // flight lose with half grids, r05zzc, and keep the whole grid)
+  // flight lose with half grids, r05zzc, and keep the whole grid).  Pixels and counts do not depend
+  // on the grid; the grid used is recorded (rt_debug_last_grid)
   if (n_frames == 1 && sc->last_ctx >= 0 && sc->last_stream != st &&
       !event_done(sc->ctx[sc->last_ctx].ev1))
     bpc = std::max(1, bpc / 2);
-  long long blocks = (long long)(sc->n_cu - sc->reserve_cus) * bpc;
-  blocks = std::max<long long>(1, std::min<long long>(blocks, (waves_needed + kBlock / 64 - 1) / (kBlock / 64)));
-  blocks = std::min<long long>(blocks, (long long)(sc->nslots / kBlock));
-  if (sc->grid_spare > 0)   // leave block slots to concurrent kernels (upload option)
-    blocks = std::max<long long>(1, blocks - sc->grid_spare);
+  const long long blocks = grid_of(bpc);
 
-  // the context's previous launch done (device side) and its staged copy consumed (host side); a
-  // launch eight back has normally ended, and then no wait goes into the stream
-  // (with the events below: one frame per call 0.4130 -> 0.4089 ms kernel, 0.4295 -> 0.4265 ms call; r05p)
-  if (C.used && !event_done(C.ev1)) {
-    HIP_TRY(hipStreamWaitEvent(st, C.ev1, 0));
-    HIP_TRY(hipEventSynchronize(C.ev1));
-  }
-  // zeroed counters + frame table, one copy from the context's pinned staging
+  // zeroed counters + frame table + light table, one copy from the context's pinned staging
   std::memset(C.h_ctl, 0, kCtrBytes);
   FrameDesc* fd = reinterpret_cast<FrameDesc*>(C.h_ctl + kCtrBytes);
   for (int f = 0; f < n_frames; ++f) {
@@ -2725,7 +2771,12 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
     }
     fd[f].out = outs[f];
   }
-  HIP_TRY(hipMemcpyAsync(C.d_ctr, C.h_ctl, kCtrBytes + (size_t)n_frames * sizeof(FrameDesc), hipMemcpyHostToDevice, st));
+  double* ld = reinterpret_cast<double*>(C.h_ctl + lights_at);
+  for (int i = 0; i < p->n_lights; ++i) {
+    const rt_light* L = rt_params_light(p, i);
+    for (int k = 0; k < 3; ++k) { ld[6 * i + k] = L->position[k]; ld[6 * i + 3 + k] = L->color[k]; }
+  }
+  HIP_TRY(hipMemcpyAsync(C.d_ctr, C.h_ctl, ctl_bytes, hipMemcpyHostToDevice, st));
   if (v == 3) {   // round timeline: zeroed, so unused records read as t = 0
     const size_t tb = sc->nslots / 64 * kTlCap * kTlWords * sizeof(unsigned long long);
     if (!C.d_tl) {
@@ -2753,6 +2804,8 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   C.used = true;
   C.variant = v;
   C.waves = rows > 0 ? blocks * (kBlock / 64) : 0;
+  C.blocks = rows > 0 ? blocks : 0;
+  C.full_blocks = rows > 0 ? full_blocks : 0;
   sc->last_ctx = ci;
   sc->last_stream = st;
   sc->next_ctx = (ci + 1) % kContexts;
@@ -2777,8 +2830,7 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
     } else {
       stats->pixels = (long long)rows * p->camera.width * n_frames;
     }
-    if (c[CD_GUARD] != 0)
-      return fail(RT_ERR_HIP, "rt_launch_compute_image: persistent-loop watchdog fired (kernel bug)");
+    if (c[CD_GUARD] != 0 || guard_tripped(sc)) return fail(RT_ERR_HIP, kGuardMsg);
   }
   return RT_OK;
 }
@@ -2976,6 +3028,10 @@ int rt_launch_adaptive_frames(rt_scene* sc, const rt_render_params* p, int n_fra
 
 int rt_render_to_host(rt_scene* sc, const rt_render_params* p, void* host_out, rt_stats* stats) {
   if (!sc || !p || !host_out) return fail(RT_ERR_INVALID, "rt_render_to_host: null argument");
+  // the host buffer holds the shard's packed rows (rt_rows_in_shard): a frame-sized layout would
+  // overrun it (and the pageable path's shard-sized staging buffer)
+  if (p->flags & RT_FLAG_GLOBAL_ROWS)
+    return fail(RT_ERR_INVALID, "rt_render_to_host: RT_FLAG_GLOBAL_ROWS is not supported (the output is the packed shard)");
   HIP_TRY(hipSetDevice(sc->device));
   const int rows = rt_rows_in_shard(p);
   const size_t elem = p->out_format == RT_OUT_RGB_F64 ? sizeof(double) : sizeof(float);
@@ -3147,6 +3203,39 @@ int rt_last_kernel_ms(rt_scene* sc, float* ms) {
   const LaunchCtx& C = sc->ctx[sc->last_ctx];
   HIP_TRY(hipEventSynchronize(C.ev1));
   HIP_TRY(hipEventElapsedTime(ms, C.ev0, C.ev1));
+  if (guard_tripped(sc)) return fail(RT_ERR_HIP, kGuardMsg);
+  return RT_OK;
+}
+
+int rt_scene_status(const rt_scene* sc) {
+  if (!sc) return fail(RT_ERR_INVALID, "rt_scene_status: null scene");
+  return guard_tripped(sc) ? fail(RT_ERR_HIP, kGuardMsg) : RT_OK;
+}
+
+int rt_debug_last_grid(rt_scene* sc, long long* blocks, long long* full_blocks) {
+  if (!sc || sc->last_ctx < 0) return fail(RT_ERR_INVALID, "rt_debug_last_grid: no launch recorded");
+  const LaunchCtx& C = sc->ctx[sc->last_ctx];
+  if (blocks) *blocks = C.blocks;
+  if (full_blocks) *full_blocks = C.full_blocks;
+  return RT_OK;
+}
+
+int rt_debug_corrupt_hierarchy(rt_scene* sc) {
+  if (!sc) return fail(RT_ERR_INVALID, "rt_debug_corrupt_hierarchy: null scene");
+  if (sc->n_gnodes4 < 1) return fail(RT_ERR_INVALID, "rt_debug_corrupt_hierarchy: the scene has no 4-wide node");
+  HIP_TRY(hipSetDevice(sc->device));
+  HIP_TRY(hipDeviceSynchronize());   // launches in flight read the hierarchy
+  // node 0 becomes a cycle that never grows the stack: one child, node 0 itself, whose box holds
+  // every ray; the other slots empty ([+inf, -inf], kEmpty)
+  GNode4 n;
+  std::memset(&n, 0, sizeof n);
+  for (int c = 0; c < 4; ++c) {
+    const float lo = c == 0 ? -1e30f : INFINITY, hi = c == 0 ? 1e30f : -INFINITY;
+    n.lox[c] = n.loy[c] = n.loz[c] = lo;
+    n.hix[c] = n.hiy[c] = n.hiz[c] = hi;
+    n.ref[c] = c == 0 ? 0u : kEmpty;
+  }
+  HIP_TRY(hipMemcpy(sc->d_nodes4, &n, sizeof n, hipMemcpyHostToDevice));
   return RT_OK;
 }
 
@@ -3220,9 +3309,10 @@ void rt_scene_free(rt_scene* sc) {
   (void)hipSetDevice(sc->device);
   (void)hipDeviceSynchronize();   // launches may still be reading the scene
   void* ptrs[] = {sc->d_cost[0], sc->d_cost[1], sc->d_cost[2], sc->d_order[0], sc->d_order[1], sc->d_tile_order, sc->d_host_stage, sc->d_nodes, sc->d_nodes4, sc->d_tris, sc->d_shade, sc->d_tnorm, sc->d_tu,
-                  sc->d_tv, sc->d_texels, sc->d_mats, sc->d_lights, sc->d_slot2dev, sc->d_prims};
+                  sc->d_tv, sc->d_texels, sc->d_mats, sc->d_slot2dev, sc->d_prims};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
+  if (sc->h_guard) (void)hipHostFree(sc->h_guard);
   for (LaunchCtx& c : sc->ctx) {
     void* cp[] = {c.d_ctr, c.d_pstate, c.d_spill, c.d_wavelog, c.d_tl, c.d_wctr};
     for (void* q : cp)

@@ -67,6 +67,9 @@ class Raytracer {
         if (rt_multi_render_to_host(multi_, &params_, kStripe, image_.data(), &st, &mt) != RT_OK)
           return error(rt_multi_last_error());
         ms = (float)mt;
+        if (f == 0)   // (peer stores are kept only if the driver's bit check of the first frame passed)
+          std::printf("frame assembly in use: %s\n",
+                      rt_multi_assembly(multi_) == RT_MULTI_PEER ? "peer stores" : "RCCL gather");
       } else {
         if (rt_render_to_host(gpu_, &params_, image_.data(), &st) != RT_OK) return error(rt_last_error());
         rt_last_kernel_ms(gpu_, &ms);

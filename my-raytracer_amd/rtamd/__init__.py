@@ -408,6 +408,20 @@ class DeviceScene:
         _check_hip(hip_lib().rt_last_kernel_ms(self._h, C.byref(ms)), "rt_last_kernel_ms")
         return ms.value
 
+    def status(self):
+        """rt_scene_status: RT_OK, or RT_ERR_HIP once a finished launch tripped the kernel watchdog."""
+        return int(hip_lib().rt_scene_status(self._h))
+
+    def last_grid(self):
+        """(blocks, full_blocks) of the last launch's persistent grid (rt_debug_last_grid)."""
+        b, f = C.c_longlong(0), C.c_longlong(0)
+        _check_hip(hip_lib().rt_debug_last_grid(self._h, C.byref(b), C.byref(f)), "rt_debug_last_grid")
+        return b.value, f.value
+
+    def debug_corrupt_hierarchy(self):
+        """Test hook (rt_debug_corrupt_hierarchy): the first 4-wide node becomes a cycle."""
+        _check_hip(hip_lib().rt_debug_corrupt_hierarchy(self._h), "rt_debug_corrupt_hierarchy")
+
 
 def tile_shape():
     """(width, height) of the render kernel's work tile (rt_tile_shape)."""
@@ -511,6 +525,20 @@ class MultiScene:
             self.close()
             raise RtError(f"rt_multi_set_assembly: {err}")
         self.assembly = assembly
+
+    @property
+    def assembly_in_use(self):
+        """"gather" or "peer": the assembly rt_multi_render* use now (the peer guard falls back to
+        the gather when the peer stores did not assemble a bit-identical check frame)."""
+        a = multi_lib().rt_multi_assembly(self._h)
+        if a < 0:
+            raise RtError(f"rt_multi_assembly: {multi_lib().rt_multi_last_error().decode()}")
+        return "peer" if a == abi.RT_MULTI_PEER else "gather"
+
+    def debug_inject(self, what):
+        """Test hook (rt_multi_debug_inject): abi.RT_MULTI_DEBUG_PEER_MISMATCH, or 0."""
+        if multi_lib().rt_multi_debug_inject(self._h, int(what)) != RT_OK:
+            raise RtError(f"rt_multi_debug_inject: {multi_lib().rt_multi_last_error().decode()}")
 
     def render(self, params, stripe_height=16):
         """Synchronous render of the whole frame to host memory -> (image [H, W, 3], Stats, ms)."""

@@ -29,6 +29,7 @@ RT_FLAG_GLOBAL_ROWS = 128
 RT_IPC_HANDLE_BYTES = 64
 RT_MULTI_GATHER = 0
 RT_MULTI_PEER = 1
+RT_MULTI_DEBUG_PEER_MISMATCH = 1
 
 
 class Material(C.Structure):
@@ -192,6 +193,9 @@ HIP_SYMBOLS = {
     "rt_debug_set_tile_order": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint), C.c_longlong]),
     "rt_debug_last_tile_order": (C.c_longlong, [C.c_void_p, C.POINTER(C.c_uint), C.c_longlong]),
     "rt_debug_blocks_per_cu": (C.c_int, [C.c_void_p, C.c_int]),
+    "rt_debug_last_grid": (C.c_int, [C.c_void_p, C.POINTER(C.c_longlong), C.POINTER(C.c_longlong)]),
+    "rt_debug_corrupt_hierarchy": (C.c_int, [C.c_void_p]),
+    "rt_scene_status": (C.c_int, [C.c_void_p]),
     "rt_scene_free": (None, [C.c_void_p]),
     "rt_last_error": (C.c_char_p, []),
     "rt_build_info": (C.c_char_p, []),
@@ -221,6 +225,8 @@ MULTI_SYMBOLS = {
                                   C.POINTER(UploadOptions), C.POINTER(C.c_void_p)]),
     "rt_multi_device_count": (C.c_int, [C.c_void_p]),
     "rt_multi_set_assembly": (C.c_int, [C.c_void_p, C.c_int]),
+    "rt_multi_assembly": (C.c_int, [C.c_void_p]),
+    "rt_multi_debug_inject": (C.c_int, [C.c_void_p, C.c_int]),
     "rt_multi_render": (C.c_int, [C.c_void_p, C.POINTER(RenderParams), C.c_int, C.c_void_p, C.POINTER(Stats),
                                   C.POINTER(C.c_double)]),
     "rt_multi_render_frames": (C.c_int, [C.c_void_p, C.POINTER(RenderParams), C.c_int, C.c_int,

@@ -71,8 +71,33 @@ def test_binding_resource_vocabulary():
     assert b.binding_resource({"frac": 0.85, "l1_roof": {"frac": 0.3}})[0] == "hbm"
     assert b.binding_resource({"frac": 0.1, "l1_roof": {"frac": 0.9}, "valu_roof": {"frac": 0.5}})[0] == "l1"
     assert b.binding_resource({"frac": None, "l1_roof": None, "valu_roof": {"frac": 0.95}})[0] == "valu"
-    assert b.binding_resource({})[0] == "latency"
-    assert set(b.BOUND_VOCAB) == {"hbm", "l1", "valu", "latency"}
+    assert set(b.BOUND_VOCAB) == {"hbm", "l1", "valu", "latency", "unmeasured"}
+
+
+def test_binding_resource_unmeasured_without_its_basis():
+    # "latency" is a claim about measured fractions: with the HBM or the VALU fraction missing (an
+    # N > 1 line of a workload whose rank shape was never profiled) the bound is "unmeasured"
+    b = _bench()
+    assert b.binding_resource({})[0] == "unmeasured"
+    assert b.binding_resource({"frac": None, "l1_roof": {"frac": 0.7}, "valu_roof": {"frac": 0.5}})[0] == "unmeasured"
+    assert b.binding_resource({"frac": 0.03, "l1_roof": {"frac": 0.7}, "valu_roof": None})[0] == "unmeasured"
+    assert b.binding_resource({"frac": 0.03, "l1_roof": None, "valu_roof": {"frac": 0.5}})[0] == "latency"
+    bound, basis = b.binding_resource({"frac": None, "l1_roof": {"frac": 0.9}, "valu_roof": None})
+    assert bound == "l1" and basis["hbm_frac"] is None   # a measured roof at >= 0.8 still names itself
+
+
+def test_rank_shape_profiles_feed_n_gpu_lines():
+    # every N > 1 line of the driver's office shape finds the PMC summary of its rank shape (rank 0's
+    # launches profiled on one GPU with --rank-shape N): a numeric HBM fraction and a VALU roof
+    b = _bench()
+    key = {"scene": "office", "tris": 0, "width": 1920, "height": 1080, "spp": 1, "tree": "sbvh",
+           "sweep": 0.12, "adaptive": False, "analytic": False}
+    for n in (2, 4, 8):
+        for fpl in (10.0, 20.0):
+            pmc = b.pmc_per_frame(dict(key, n_gpus=n), fpl)
+            assert pmc is not None and pmc["read"] > 0 and pmc["write"] > 0, (n, fpl)
+            assert b.pmc_valu_roof(dict(key, n_gpus=n), fpl, 0.1e-3) is not None, n
+            assert b.pmc_wave_mix(dict(key, n_gpus=n), fpl) is not None, n
 
 
 def _launch(args, env_extra=None, timeout=240):

@@ -1,0 +1,16 @@
+#!/bin/bash
+# rocprofv3 summaries of the N-GPU rank shapes on one GPU (dev tool, under gpurun): bench.py
+# --rank-shape N renders exactly rank 0's launches of an N-GPU run, so the committed summary (its
+# workload_key carries n_gpus = N) gives the N > 1 bench lines their roofline (bench.py
+# pmc_per_frame).  The driver's command shape: --steps 20 --warmup 5 (gather: 10 frames per launch,
+# two in flight).   usage: bash tools/profile_rank_shapes.sh TAG [N ...]
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}"
+TAG=${1:?tag}; shift
+NS=${*:-2 4 8}
+export CALIB=profiles/r02/hbm_calib.json
+export PASSES="fetch write td sq sqa valu"
+for n in $NS; do
+  bash tools/profile_round.sh ${TAG}_n$n --rank-shape $n --steps 20 --warmup 5 --single-frames 0 \
+    || { echo "profile n=$n failed"; exit 1; }
+done

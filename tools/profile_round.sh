@@ -14,8 +14,11 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pro
 # the traced run prints its own bench line: compare per-shape kernel durations with its HIP events
 grep '^{' $O/prof_$TAG.log | tail -1 > $O/prof_${TAG}_bench.json
 python tools/trace_summary.py $O/trace_$TAG.json $O/prof_$TAG $O/prof_${TAG}_bench.json > /dev/null
+# PASSES (optional): the pass names to run (default all); the summary takes the passes that ran
+PASSES=${PASSES:-fetch write td ta tcc tcp sq sqa valu}
 pass() {
   local name=$1; shift
+  case " $PASSES " in *" $name "*) ;; *) return 0 ;; esac
   timeout -k 10 300 rocprofv3 --pmc "$@" --output-format csv -d $O/pmc_${TAG}_$name -o run -- $B > $O/pmc_${TAG}_$name.log 2>&1
 }
 pass fetch FETCH_SIZE
@@ -37,6 +40,5 @@ if [ ! -f $CAL ]; then
 fi
 # (the passes of this tag only: a glob pmc_${TAG}_*/ would also take those of a tag that extends it)
 python tools/pmc_summary.py $O/pmc_$TAG.json --bench $O/bench_$TAG.json --calib $CAL \
-  $O/pmc_${TAG}_fetch $O/pmc_${TAG}_write $O/pmc_${TAG}_td $O/pmc_${TAG}_ta $O/pmc_${TAG}_tcc $O/pmc_${TAG}_tcp \
-  $O/pmc_${TAG}_sq $O/pmc_${TAG}_sqa $O/pmc_${TAG}_valu
+  $(for p in $PASSES; do echo $O/pmc_${TAG}_$p; done)
 echo "profile $TAG done"
