@@ -244,7 +244,11 @@ typedef struct rt_upload_options {
                             the largest recorded cost within +-order_window tiles of its row; 0 = by size (4,
                             exact costs for hierarchies from 2^18 device records on, whatever stack_ring forces;
                             default), -1 = exact */
-  int reserved_[6];
+  int spp_lanes;         /* n x n > 1 samples per pixel: 1 = a pixel's samples on neighbouring lanes of one wave
+                            (groups of G = min(n^2, 64) lanes, summed in sample order on chip, n^2 a power of
+                            two), -1 = one lane per pixel, its samples in sequence; 0 = the default (DESIGN.md
+                            §11.6).  Pixels and ray counts are identical either way */
+  int reserved_[5];
 } rt_upload_options;
 
 /* Fills *opt with the defaults listed above. */

@@ -93,7 +93,9 @@ static_assert((kShortStack & kStackMask) == 0, "the stack ring must be a power o
 // batch of shadow rays in flight).  Idle lanes (FETCH / DONE) may be lent to an
 // owner of the same wave for one round (HSHADOW / HCLOSEST): they trace one of its
 // extra shadow rays or its reflection ray, so a bounce costs one round, not 1 + lights.
-enum : int { ST_FETCH = 0, ST_CLOSEST = 1, ST_SHADOW = 2, ST_DONE = 3, ST_HSHADOW = 4, ST_HCLOSEST = 5 };
+// PARKED (sample groups, spp > 1): the lane's sample is finished and its colour waits in the lane's
+// slot for its group's ordered sum (below); a parked lane is neither busy nor idle.
+enum : int { ST_FETCH = 0, ST_CLOSEST = 1, ST_SHADOW = 2, ST_DONE = 3, ST_PARKED = 4, ST_HSHADOW = 5, ST_HCLOSEST = 6 };
 constexpr uint32_t kTaskNone = 0xffffffffu;
 // task word: owner lane | (light - owner's first light of the batch) << 6 | light << 11, or
 // owner lane | kTaskRefl.  The helper derives its ray itself at the start of the traversal from
@@ -257,6 +259,10 @@ struct KParams {
   int n_lights, max_depth;
   double bg[3], amb[3];
   int spp_n;
+  // sample groups (spp > 1, rt_upload_options.spp_lanes): a pixel's samples run on G = 2^group_log
+  // neighbouring lanes of one wave, `chunks` x G samples in all (0: one lane per pixel, its samples in
+  // sequence)
+  int group_log, chunks;
   int row_begin, stripe_h, stripe_count, stripe_index;
   int rows;
   int tiles_x;
@@ -563,7 +569,13 @@ __device__ __forceinline__ uint32_t u4c(const uint4& v, int c) {
 }
 
 
-constexpr int kWavesPerEU = 4;   // 4 waves/SIMD = 16 waves/CU (register budget 128 VGPRs)
+// 4 waves/SIMD = 16 waves/CU (register budget 128 VGPRs); measurement builds may ask for 5
+// (make variant V="-DRT_WAVES_PER_EU=5": 96 VGPRs, spills; 5 blocks per CU also need <= 32 KB of LDS:
+// upload option lds_treelet=9)
+#ifndef RT_WAVES_PER_EU
+#define RT_WAVES_PER_EU 4
+#endif
+constexpr int kWavesPerEU = RT_WAVES_PER_EU;
 
 // RING: entries of the per-lane traversal-stack ring in LDS (8: room for the 73-node treelet;
 // 16: deep hierarchies, e.g. millions of random triangles, which spill an 8-entry ring often;
@@ -673,7 +685,26 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
   uint32_t* spill = P.spill + (size_t)blockIdx.x * kBlock + threadIdx.x;
 
   const int lane = threadIdx.x & 63;
-  const unsigned long long lane_below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  // bit `lane` of a wave-uniform mask (lane opaque at the use: the compiler would otherwise hold a
+  // 64-bit 1 << lane in registers across the loop)
+  auto lane_bit = [&](unsigned long long m) -> bool {
+    int l = lane;
+    asm volatile("" : "+v"(l));
+    return ((m >> l) & 1ull) != 0ull;
+  };
+  // lanes of mask m below this lane: v_mbcnt (no 64-bit lane mask held in registers)
+  auto below = [](unsigned long long m) -> int {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  };
+  // sample groups: of a wave mask m, the first-lane bits of the groups whose G lanes are all set
+  // (wave-uniform; G a power of two <= 64)
+  auto full_groups = [&](unsigned long long m) -> unsigned long long {
+    const int gl = P.group_log;
+    for (int sh = 1; sh < (1 << gl); sh <<= 1) m &= m >> sh;
+    unsigned long long first = 0ull;   // bit 0 of every group
+    for (int b = 0; b < 64; b += 1 << gl) first |= 1ull << b;
+    return m & first;
+  };
   // path state, [wave][region][64 lanes][4 fp64] (see kRegions): b128 buffer ops with the lane
   // offset in one VGPR and the region offset as an SGPR constant.
   const __amdgpu_buffer_rsrc_t prs =
@@ -801,7 +832,8 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
 
   // primary ray of the current sample (mytracer_gpu.cu:202-209; Camera::primary_ray)
   auto start_sample = [&]() {
-    const int n = P.spp_n;
+    int n = P.spp_n;
+    asm volatile("" : "+s"(n));   // not hoisted: the fp64 offsets below stay temporaries of this block
     double X, Y;
     if (n == 1) {   // xo = 0/1 - 0.5 + 1/2 = +0 exactly: X = px + 0 = px
       X = (double)px;
@@ -824,6 +856,44 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
     emit_ray(d3(K.eye[0], K.eye[1], K.eye[2]), dir, DBL_MAX);
     state = ST_CLOSEST;
   };
+  // compute_image's last step for the pixel (px, lrow, frame): average the sum over the n x n
+  // samples, clamp, store (mytracer_gpu.cu:155-159, 221-227)
+  auto store_pixel = [&](D3 pcol) {
+    int n2 = P.spp_n * P.spp_n;
+    asm volatile("" : "+s"(n2));   // converted here, not hoisted into a VGPR live across the loop
+    const double nn = (double)n2;
+    double r, g, b;
+    if ((n2 & (n2 - 1)) == 0) {
+      // n2 = 2^k: x / n2 = x * 2^-k exactly (one rounding of the same exact value), no division
+      const double s = __builtin_ldexp(1.0, -__builtin_ctz((unsigned)n2));
+      r = stdmin(pcol.x * s, 1.0); g = stdmin(pcol.y * s, 1.0); b = stdmin(pcol.z * s, 1.0);
+    } else {
+      r = stdmin(pcol.x / nn, 1.0); g = stdmin(pcol.y / nn, 1.0); b = stdmin(pcol.z / nn, 1.0);
+    }
+    // RT_FLAG_GLOBAL_ROWS: the row's place in the whole frame (the buffer may be another GPU's,
+    // mapped over xGMI: the shard's pixels land in the assembled frame as they finish)
+    const int orow = P.out_global ? (P.stripe_count == 1 ? P.row_begin + lrow : stripe_row(P, lrow)) : lrow;
+    const size_t o = 3 * ((size_t)orow * P.W + px);
+    // nontemporal (evict-first): the frame is written once and never read here, so its lines
+    // should not push the path-state lines out of L2 (office: HBM writes 50.9 -> 45.5 MB per
+    // frame, time unchanged; profiles/r03/write_traffic_r03.json)
+#ifdef RT_MEAS_NO_IMAGE   // write-attribution build: no image stores
+    if (false)
+#else
+    if (P.out_fmt == RT_OUT_RGB_F64)
+#endif
+    {
+      double* out = reinterpret_cast<double*>(P.frames[frame].out) + o;
+      __builtin_nontemporal_store(r, out); __builtin_nontemporal_store(g, out + 1);
+      __builtin_nontemporal_store(b, out + 2);
+    } else {
+#ifndef RT_MEAS_NO_IMAGE
+      float* out = reinterpret_cast<float*>(P.frames[frame].out) + o;
+      __builtin_nontemporal_store((float)r, out); __builtin_nontemporal_store((float)g, out + 1);
+      __builtin_nontemporal_store((float)b, out + 2);
+#endif
+    }
+  };
 
   unsigned guard = 0;
   for (;;) {
@@ -835,11 +905,14 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
     // ---------------- refill idle lanes (one atomic per wave) ----------------
     unsigned long long m_fetch = wballot(state == ST_FETCH);
     unsigned long long m_busy = wballot(state == ST_CLOSEST || state == ST_SHADOW || state >= ST_HSHADOW);
-    while (m_fetch && (__popcll(m_fetch) >= kRefill || m_busy == 0) && heads_left > 0) {
+    // lanes that claim a work item: every idle lane, or (sample groups) the first lane of every idle
+    // group, which claims a pixel for its G lanes
+    unsigned long long m_claim = P.group_log ? full_groups(m_fetch) : m_fetch;
+    while (m_claim && (P.group_log || __popcll(m_fetch) >= kRefill || m_busy == 0) && heads_left > 0) {
       const long long g0 = (n_tiles * head / kGroups) * 64;
       const long long g1 = (n_tiles * (head + 1) / kGroups) * 64;
-      const int cnt = __popcll(m_fetch);
-      const int leader = __ffsll((long long)m_fetch) - 1;
+      const int cnt = __popcll(m_claim);
+      const int leader = __ffsll((long long)m_claim) - 1;
       if ((*pool_exh >> head) & 1u) {   // another wave of the block found it exhausted
         head = (head + 1) % kGroups;
         heads_left--;
@@ -856,15 +929,23 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
         continue;
       }
       if (STATS) { w_refill = __builtin_amdgcn_s_memrealtime(); w_pixels += (unsigned long long)min((long long)cnt, g1 - start); }
-      if (state == ST_FETCH) {
-        const long long wk = start + __popcll(m_fetch & lane_below);
+      // this lane's item: its rank among the claiming lanes (sample groups: its group's rank)
+      const int gbase = P.group_log ? (lane & ~((1 << P.group_log) - 1)) : lane;
+      const bool claims = state == ST_FETCH && (!P.group_log || ((m_claim >> gbase) & 1ull) != 0ull);
+      if (claims) {
+        const long long wk = start + (P.group_log ? __popcll(m_claim & ((1ull << gbase) - 1ull)) : below(m_fetch));
         if (wk < g1) {
           if (P.list) {   // adaptive pass: one sample of a listed pixel
-            const uint32_t id = wk < n_list ? P.list[wk / P.nsamp] : 0xffffffffu;
+            // (the divisors made opaque here: the compiler would otherwise keep their reciprocals in
+            // registers across the whole persistent loop)
+            long long ns = P.nsamp;
+            uint32_t wd = (uint32_t)P.W;
+            asm volatile("" : "+s"(ns), "+s"(wd));
+            const uint32_t id = wk < n_list ? P.list[wk / ns] : 0xffffffffu;
             const uint32_t pix = id & kListPixMask;
             frame = id != 0xffffffffu ? (int)(id >> kListFrameShift) : 0;
-            px = id != 0xffffffffu ? (int)(pix % (uint32_t)P.W) : P.W;
-            lrow = id != 0xffffffffu ? (int)(pix / (uint32_t)P.W) : P.rows;
+            px = id != 0xffffffffu ? (int)(pix % wd) : P.W;
+            lrow = id != 0xffffffffu ? (int)(pix / wd) : P.rows;
             item = wk;
           } else {
             // (tile indices < 2^31, checked at launch: 32-bit divisions by the launch's invariant
@@ -885,14 +966,21 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
             py = (P.stripe_count == 1)
                      ? P.row_begin + lrow
                      : stripe_row(P, lrow);
-            sample = P.list ? (int)(item % P.nsamp) : 0;
+            if (P.list) {
+              long long ns = P.nsamp;
+              asm volatile("" : "+s"(ns));
+              sample = (int)(item % ns);
+            } else {
+              sample = lane - gbase;   // sample groups: the lane's place in its group (chunk 0); else 0
+            }
             start_sample();
           }
         }
       }
       m_fetch = wballot(state == ST_FETCH);
       m_busy = wballot(state == ST_CLOSEST || state == ST_SHADOW || state >= ST_HSHADOW);
-      if (__popcll(m_fetch) < kRefill && m_busy != 0) break;
+      m_claim = P.group_log ? full_groups(m_fetch) : m_fetch;
+      if (!P.group_log && __popcll(m_fetch) < kRefill && m_busy != 0) break;
     }
     if (heads_left == 0 && state == ST_FETCH) state = ST_DONE;
     const bool busy = (state == ST_CLOSEST || state == ST_SHADOW || state >= ST_HSHADOW);
@@ -1408,7 +1496,8 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
     }
 
     // ---- tail compaction: donate (sparse wave, queue empty) or adopt pooled lanes ----
-    if (heads_left == 0) {
+    // (not with sample groups: a group's lanes and their parked colours stay in their wave)
+    if (heads_left == 0 && !P.group_log) {
       // wave in block, wave-uniform (an SGPR: derived at the use, not a VGPR held across the loop)
       const int wib = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
       const bool owner = (state == ST_CLOSEST || state == ST_SHADOW);
@@ -1448,7 +1537,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
         unsigned long long back = 0ull;
         if (lane == 0) back = atomicAnd(&pool_mask[wib], 0ull);
         back = __shfl(back, 0);
-        if (owner && !((back >> lane) & 1ull)) state = ST_DONE;   // adopted by another wave
+        if (owner && !lane_bit(back)) state = ST_DONE;   // adopted by another wave
       } else {
         // adopt pooled lanes of other waves into idle lanes
         unsigned long long I = wballot((state == ST_FETCH || state == ST_DONE) && !refl_held);
@@ -1468,8 +1557,8 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
           const int n = __popcll(got);
           if (n == 0) continue;
           // the r-th idle lane takes the r-th adopted lane of donor wave w
-          const bool idle = (I >> lane) & 1ull;
-          const int r = __popcll(I & lane_below);
+          const bool idle = lane_bit(I);
+          const int r = below(I);
           const bool take = idle && r < n;
           if (take) {
             const int t = w * 64 + kth_set_bit(got, r);   // donor thread
@@ -1694,6 +1783,10 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
         double* so = P.sample_out + 3 * (size_t)item;
         so[0] = c.x; so[1] = c.y; so[2] = c.z;
         state = heads_left > 0 ? ST_FETCH : ST_DONE;
+      } else if (finish && P.group_log) {
+        // sample groups: the colour waits in the (now free) ray slot for the group's ordered sum
+        *R.o[0] = scol.x; *R.o[1] = scol.y; *R.o[2] = scol.z;
+        state = ST_PARKED;
       } else if (finish) {
         if (P.tile_cost) {   // cost of this sample: its bounces, or in time mode the pixel's lifetime at its
                              // last sample, summed per tile position over the launch's frames
@@ -1725,45 +1818,41 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
           STV(R_PCOL, pcol);
           start_sample();
         } else {   // compute_image: average, clamp, store (mytracer_gpu.cu:155-159, 221-227)
-          int n2 = P.spp_n * P.spp_n;
-          asm volatile("" : "+s"(n2));   // converted here, not hoisted into a VGPR live across the loop
-          const double nn = (double)n2;
-          double r, g, b;
-          if ((n2 & (n2 - 1)) == 0) {
-            // n2 = 2^k: x / n2 = x * 2^-k exactly (one rounding of the same exact value), no division
-            const double s = __builtin_ldexp(1.0, -__builtin_ctz((unsigned)n2));
-            r = stdmin(pcol.x * s, 1.0); g = stdmin(pcol.y * s, 1.0); b = stdmin(pcol.z * s, 1.0);
-          } else {
-            r = stdmin(pcol.x / nn, 1.0); g = stdmin(pcol.y / nn, 1.0); b = stdmin(pcol.z / nn, 1.0);
-          }
-          // RT_FLAG_GLOBAL_ROWS: the row's place in the whole frame (the buffer may be another GPU's,
-          // mapped over xGMI: the shard's pixels land in the assembled frame as they finish)
-          const int orow = P.out_global ? (P.stripe_count == 1 ? P.row_begin + lrow : stripe_row(P, lrow)) : lrow;
-          const size_t o = 3 * ((size_t)orow * P.W + px);
-          // nontemporal (evict-first): the frame is written once and never read here, so its lines
-          // should not push the path-state lines out of L2 (office: HBM writes 50.9 -> 45.5 MB per
-          // frame, time unchanged; profiles/r03/write_traffic_r03.json)
-#ifdef RT_MEAS_NO_IMAGE   // write-attribution build: no image stores
-          if (false)
-#else
-          if (P.out_fmt == RT_OUT_RGB_F64)
-#endif
-          {
-            double* out = reinterpret_cast<double*>(P.frames[frame].out) + o;
-            __builtin_nontemporal_store(r, out); __builtin_nontemporal_store(g, out + 1);
-            __builtin_nontemporal_store(b, out + 2);
-          } else {
-#ifndef RT_MEAS_NO_IMAGE
-            float* out = reinterpret_cast<float*>(P.frames[frame].out) + o;
-            __builtin_nontemporal_store((float)r, out); __builtin_nontemporal_store((float)g, out + 1);
-            __builtin_nontemporal_store((float)b, out + 2);
-#endif
-          }
+          store_pixel(pcol);
           state = heads_left > 0 ? ST_FETCH : ST_DONE;
         }
       }
     }
     asm volatile("" ::: "memory");
+
+    // ---- sample groups: a group whose G samples are all parked is summed by its first lane ----
+    // in sample order (the reference's (si, sj) order, mytracer_gpu.cu:202-221: sample s = si n + sj,
+    // and a group holds samples chunk * G .. chunk * G + G - 1 on its lanes in order), then the group
+    // starts its next chunk, or the pixel is stored and the group fetches another
+    if (P.group_log) {
+      const unsigned long long full = full_groups(wballot(state == ST_PARKED));
+      if (full != 0ull) {
+        wave_lds_sync();   // the group's colours, written by its lanes in SHADE, are in LDS
+        const int gl = P.group_log;
+        const int gbase = lane & ~((1 << gl) - 1);
+        const bool group_done = ((full >> gbase) & 1ull) != 0ull;
+        if (group_done && lane == gbase) {
+          D3 pc = sample == 0 ? d3(0, 0, 0) : LDV(R_PCOL);   // (the first lane holds sample chunk * G)
+          for (int k = 0; k < (1 << gl); ++k) {
+            const int t = wbase + gbase + k;
+            pc = add(pc, d3(lds_d[0 * kBlock + t], lds_d[1 * kBlock + t], lds_d[2 * kBlock + t]));
+          }
+          if (sample + (1 << gl) < P.spp_n * P.spp_n) STV(R_PCOL, pc);   // more chunks: the running sum
+          else store_pixel(pc);
+        }
+        wave_lds_sync();   // the first lane has read the group's slots before they take new rays
+        if (group_done) {
+          sample += 1 << gl;
+          if (sample < P.spp_n * P.spp_n) start_sample();
+          else state = heads_left > 0 ? ST_FETCH : ST_DONE;
+        }
+      }
+    }
 
     // ---- lend idle lanes to owners' extra rays (extra lights in order, then reflection) ----
     {
@@ -2068,6 +2157,8 @@ const Variant kVariants[] = {
     {render_kernel<4, false, false, 16>, false},
 };
 constexpr int kNumVariants = 5;
+// rt_upload_options.spp_lanes = 0: sample groups for spp > 1 launches or not
+constexpr bool kSppLanesDefault = false;
 constexpr int kRingDeep = 16;
 inline int variant_ring(int v) { return v == 4 ? kRingDeep : kShortStack; }
 // LDS per block: the variant's stack ring (ring entries per thread, at address 0: the kernel's
@@ -2182,6 +2273,7 @@ struct rt_scene {
   // CUs free, one per caller stream (at most kMaskedStreams; further callers share slot hash % 4)
   int reserve_cus = 0;
   int order_window = 0;   // rt_upload_options.order_window (0: by depth)
+  int spp_lanes = 0;      // rt_upload_options.spp_lanes (sample groups for spp > 1)
   static constexpr int kMaskedStreams = 4;
   hipStream_t masked[kMaskedStreams] = {};
   hipStream_t masked_for[kMaskedStreams] = {};
@@ -2276,6 +2368,7 @@ int upload_image(const SceneImage& I, const rt_upload_options& opt, int device, 
   sc->grid_spare = opt.grid_spare;
   sc->reserve_cus = opt.reserve_cus;   // bounded by the CU count below
   sc->order_window = opt.order_window;
+  sc->spp_lanes = opt.spp_lanes;
   sc->delta = I.delta;
   for (int k = 0; k < 3; ++k) {
     sc->root_lo[k] = I.root_lo[k];
@@ -2351,6 +2444,7 @@ int resolve_options(const rt_upload_options* opt, rt_upload_options& o) {
   if (o.reserve_cus < -1) return fail(RT_ERR_INVALID, "rt_scene_upload: reserve_cus must be >= -1");
   if (o.order_window < -1 || o.order_window > 64)
     return fail(RT_ERR_INVALID, "rt_scene_upload: order_window must be in [-1, 64]");
+  if (o.spp_lanes < -1 || o.spp_lanes > 1) return fail(RT_ERR_INVALID, "rt_scene_upload: spp_lanes must be -1, 0 or 1");
   if (o.stack_ring != 0 && o.stack_ring != 8 && o.stack_ring != 16)
     return fail(RT_ERR_INVALID, "rt_scene_upload: stack_ring must be 0, 8 or 16");
   if (o.blocks_per_cu < 0 || o.grid_spare < 0 || o.build_threads < 0)
@@ -2668,8 +2762,19 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
       !(p->flags & (RT_FLAG_TRAVERSAL_STATS | RT_FLAG_WIDE_STATS | RT_FLAG_TIMELINE | RT_FLAG_TILE_COST |
                     RT_FLAG_TILE_COST_TIME | RT_FLAG_NATURAL_ORDER)) &&
       !debug_order && (!sc->maps_used || sc->maps_stream == st);
-  const bool cost_order = !list && n_frames == 1 && ((p->flags & RT_FLAG_COST_ORDER) || implicit_order);
   const bool cost_debug = !list && (p->flags & (RT_FLAG_TILE_COST | RT_FLAG_TILE_COST_TIME));
+  // sample groups (spp > 1): a pixel's samples on G = min(n^2, 64) neighbouring lanes, n^2 a power of
+  // two (groups tile the wave), summed in order on chip; the tile-cost maps record per-lane pixel
+  // costs, so launches that record or use them keep one lane per pixel
+  const bool group = !list && !cost_debug && P.nsamp > 1 && (P.nsamp & (P.nsamp - 1)) == 0 &&
+                     (sc->spp_lanes > 0 || (sc->spp_lanes == 0 && kSppLanesDefault)) &&
+                     !(p->flags & RT_FLAG_COST_ORDER);
+  if (group) {
+    P.group_log = 0;
+    while ((1 << (P.group_log + 1)) <= std::min(P.nsamp, 64)) P.group_log++;
+    P.chunks = P.nsamp >> P.group_log;
+  }
+  const bool cost_order = !list && !group && n_frames == 1 && ((p->flags & RT_FLAG_COST_ORDER) || implicit_order);
   if (cost_order || cost_debug) {
     const long long n_pos = (long long)P.tiles_x * ((rows + kTileH - 1) / kTileH);
     if (sc->cost_cap < n_pos) {

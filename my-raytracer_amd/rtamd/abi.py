@@ -149,7 +149,8 @@ class UploadOptions(C.Structure):
                 ("sbvh_bins", C.c_int), ("blocks_per_cu", C.c_int), ("grid_spare", C.c_int),
                 ("verbose", C.c_int), ("sbvh_alpha", C.c_double), ("sbvh_budget", C.c_double),
                 ("sbvh_c_trav", C.c_double), ("collapse_c_tri", C.c_double), ("reserve_cus", C.c_int),
-                ("order_window", C.c_int), ("reserved_", C.c_int * 6)]
+                ("order_window", C.c_int), ("spp_lanes", C.c_int),
+                ("reserved_", C.c_int * 5)]
 
 
 RT_TREE_SAH, RT_TREE_REFERENCE, RT_TREE_SBVH = 0, 1, 2

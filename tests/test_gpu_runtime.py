@@ -64,15 +64,15 @@ def test_watchdog_reported_by_launch_without_stats(office):
 def test_lights_change_per_call_on_three_streams(office):
     # Every launch stages its own light table (the reference copies lights per call,
     # mytracer.cpp:105-118): launches on 3 streams, lights different in every call (inline tables
-    # and lights_ext beyond RT_MAX_LIGHTS, which grows a context's control block), nothing
-    # synchronised in between -- each result equals its serial render bit for bit.
+    # and lights_ext beyond RT_MAX_LIGHTS), nothing synchronised in between -- each result equals
+    # its serial render bit for bit.
     import torch
 
     hs, dev = office
     jobs = []
     for k in range(9):
         p = _natural(hs.render_params(160, 90, 1), rtamd.RT_OUT_RGB_F64)
-        n = (2, 5, 20)[k % 3]
+        n = (2, 20, 400)[k % 3]   # 400 lights (lights_ext) outgrow a context's control block: it grows
         lights = []
         for i in range(n):
             a = 0.7 * k + 2.0 * np.pi * i / n
@@ -192,3 +192,43 @@ def test_multi_calls_keep_the_current_device(office):
     assert torch.cuda.current_device() == before and img.shape == (24, 32, 3)
     m.close()
     assert torch.cuda.current_device() == before
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 8, 16])
+def test_sample_groups_equal_lane_per_pixel(office, n):
+    # spp_lanes = 1: a pixel's n x n samples run on neighbouring lanes of one wave (groups of
+    # min(n^2, 64) lanes; n^2 = 256: four chunks of 64 with the running sum in the path state) and are
+    # summed in sample order on chip; n = 3 (9 samples, not a power of two) keeps one lane per pixel.
+    # Pixels and ray counts equal the lane-per-pixel render bit for bit -- one frame, several frames
+    # in one launch, a striped shard -- and the oracle within the fp64 tolerance.
+    import torch
+    import pyoracle
+
+    hs, _ = office
+    on, off = rtamd.DeviceScene(hs, 0, spp_lanes=1), rtamd.DeviceScene(hs, 0, spp_lanes=-1)
+    w, h = (64, 40) if n <= 8 else (24, 16)
+    p = hs.render_params(w, h, n)
+    p.out_format = rtamd.RT_OUT_RGB_F64
+    a, sa = on.render(p)
+    b, sb = off.render(p)
+    assert np.array_equal(a, b) and [sa.primary_rays, sa.shadow_rays, sa.reflection_rays] == \
+        [sb.primary_rays, sb.shadow_rays, sb.reflection_rays]
+    if n == 4:
+        ref, cnt = pyoracle.Oracle(hs.raw, hs).render(p, pyoracle.MODE_REFERENCE)
+        assert np.abs(a - ref).max() <= 1e-12 and sa.primary_rays == cnt.primary_rays
+    cams = []
+    for f in range(3):
+        c = rtamd.camera_orbit(p, 0.05 * f)
+        c.stripe_height, c.stripe_count, c.stripe_index = 4, 3, 1
+        cams.append(c)
+    rows = rtamd.rows_in_shard(cams[0])
+    outs = {k: [torch.full((rows, w, 3), float("nan"), dtype=torch.float64, device="cuda") for _ in cams]
+            for k in ("on", "off")}
+    st_on = on.launch_frames(cams, [o.data_ptr() for o in outs["on"]], stats=True)
+    st_off = off.launch_frames(cams, [o.data_ptr() for o in outs["off"]], stats=True)
+    for x, y in zip(outs["on"], outs["off"]):
+        assert torch.equal(x, y)
+    assert st_on.primary_rays + st_on.shadow_rays + st_on.reflection_rays == \
+        st_off.primary_rays + st_off.shadow_rays + st_off.reflection_rays
+    on.close()
+    off.close()
