@@ -244,10 +244,12 @@ typedef struct rt_upload_options {
                             the largest recorded cost within +-order_window tiles of its row; 0 = by size (4,
                             exact costs for hierarchies from 2^18 device records on, whatever stack_ring forces;
                             default), -1 = exact */
-  int spp_lanes;         /* n x n > 1 samples per pixel: 1 = a pixel's samples on neighbouring lanes of one wave
-                            (groups of G = min(n^2, 64) lanes, summed in sample order on chip, n^2 a power of
-                            two), -1 = one lane per pixel, its samples in sequence; 0 = the default (DESIGN.md
-                            §11.6).  Pixels and ray counts are identical either way */
+  int spp_lanes;         /* n x n > 1 samples per pixel, n^2 a power of two: 1 = a pixel's samples on
+                            neighbouring lanes of one wave (groups of G = min(n^2, 64) lanes, summed in sample
+                            order on chip), -1 = one lane per pixel, its samples in sequence; 0 = the default,
+                            groups (4K 16 spp +22.6 %, 8K 64 spp +19.3 %).  Launches with
+                            other n, the diagnostic flags, tile-cost maps or RT_FLAG_COST_ORDER keep one lane
+                            per pixel.  Pixels and ray counts are identical either way */
   int reserved_[5];
 } rt_upload_options;
 
@@ -409,7 +411,8 @@ int rt_debug_counters(rt_scene* scene, unsigned long long* out, int n);
 long long rt_debug_wave_log(rt_scene* scene, unsigned long long* out, long long n);
 
 /* Diagnostics: persistent-grid blocks per CU of kernel variant 0 (production), 1 (4-wide
- * STATS), 2 (2-wide canonical STATS) or 3 (timeline), as the launches use it. */
+ * STATS), 2 (2-wide canonical STATS), 3 (timeline), 4 (production, 16-entry stack ring), 5 / 6
+ * (0 / 4 with sample groups, spp > 1), as the launches use it. */
 int rt_debug_blocks_per_cu(rt_scene* scene, int variant);
 
 /* Diagnostics: the persistent grid (blocks) the last launch on the scene used, and the grid a

@@ -631,7 +631,7 @@ __device__ void order_range(const uint32_t* cost, uint32_t* order, long long n_t
   }
 }
 
-template <int WIDTH, bool STATS, bool TL = false, int RING = kShortStack>
+template <int WIDTH, bool STATS, bool TL = false, int RING = kShortStack, bool GRP = false>
 __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_kernel(KParams P) {
   static_assert(RING >= kMigWords && (RING & (RING - 1)) == 0, "ring: a power of two holding the migration words");
   constexpr int kRingMask = RING - 1;
@@ -696,10 +696,12 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
   auto below = [](unsigned long long m) -> int {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
   };
+  // sample groups (the GRP variants only: the others compile none of it): log2 G, 0 = off
+  const int group_log = GRP ? P.group_log : 0;
   // sample groups: of a wave mask m, the first-lane bits of the groups whose G lanes are all set
   // (wave-uniform; G a power of two <= 64)
   auto full_groups = [&](unsigned long long m) -> unsigned long long {
-    const int gl = P.group_log;
+    const int gl = group_log;
     for (int sh = 1; sh < (1 << gl); sh <<= 1) m &= m >> sh;
     unsigned long long first = 0ull;   // bit 0 of every group
     for (int b = 0; b < 64; b += 1 << gl) first |= 1ull << b;
@@ -907,8 +909,8 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
     unsigned long long m_busy = wballot(state == ST_CLOSEST || state == ST_SHADOW || state >= ST_HSHADOW);
     // lanes that claim a work item: every idle lane, or (sample groups) the first lane of every idle
     // group, which claims a pixel for its G lanes
-    unsigned long long m_claim = P.group_log ? full_groups(m_fetch) : m_fetch;
-    while (m_claim && (P.group_log || __popcll(m_fetch) >= kRefill || m_busy == 0) && heads_left > 0) {
+    unsigned long long m_claim = group_log ? full_groups(m_fetch) : m_fetch;
+    while (m_claim && (group_log || __popcll(m_fetch) >= kRefill || m_busy == 0) && heads_left > 0) {
       const long long g0 = (n_tiles * head / kGroups) * 64;
       const long long g1 = (n_tiles * (head + 1) / kGroups) * 64;
       const int cnt = __popcll(m_claim);
@@ -930,10 +932,10 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
       }
       if (STATS) { w_refill = __builtin_amdgcn_s_memrealtime(); w_pixels += (unsigned long long)min((long long)cnt, g1 - start); }
       // this lane's item: its rank among the claiming lanes (sample groups: its group's rank)
-      const int gbase = P.group_log ? (lane & ~((1 << P.group_log) - 1)) : lane;
-      const bool claims = state == ST_FETCH && (!P.group_log || ((m_claim >> gbase) & 1ull) != 0ull);
+      const int gbase = group_log ? (lane & ~((1 << group_log) - 1)) : lane;
+      const bool claims = state == ST_FETCH && (!group_log || ((m_claim >> gbase) & 1ull) != 0ull);
       if (claims) {
-        const long long wk = start + (P.group_log ? __popcll(m_claim & ((1ull << gbase) - 1ull)) : below(m_fetch));
+        const long long wk = start + (group_log ? __popcll(m_claim & ((1ull << gbase) - 1ull)) : below(m_fetch));
         if (wk < g1) {
           if (P.list) {   // adaptive pass: one sample of a listed pixel
             // (the divisors made opaque here: the compiler would otherwise keep their reciprocals in
@@ -979,8 +981,8 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
       }
       m_fetch = wballot(state == ST_FETCH);
       m_busy = wballot(state == ST_CLOSEST || state == ST_SHADOW || state >= ST_HSHADOW);
-      m_claim = P.group_log ? full_groups(m_fetch) : m_fetch;
-      if (!P.group_log && __popcll(m_fetch) < kRefill && m_busy != 0) break;
+      m_claim = group_log ? full_groups(m_fetch) : m_fetch;
+      if (!group_log && __popcll(m_fetch) < kRefill && m_busy != 0) break;
     }
     if (heads_left == 0 && state == ST_FETCH) state = ST_DONE;
     const bool busy = (state == ST_CLOSEST || state == ST_SHADOW || state >= ST_HSHADOW);
@@ -1497,7 +1499,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
 
     // ---- tail compaction: donate (sparse wave, queue empty) or adopt pooled lanes ----
     // (not with sample groups: a group's lanes and their parked colours stay in their wave)
-    if (heads_left == 0 && !P.group_log) {
+    if (heads_left == 0 && !group_log) {
       // wave in block, wave-uniform (an SGPR: derived at the use, not a VGPR held across the loop)
       const int wib = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
       const bool owner = (state == ST_CLOSEST || state == ST_SHADOW);
@@ -1783,7 +1785,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
         double* so = P.sample_out + 3 * (size_t)item;
         so[0] = c.x; so[1] = c.y; so[2] = c.z;
         state = heads_left > 0 ? ST_FETCH : ST_DONE;
-      } else if (finish && P.group_log) {
+      } else if (finish && group_log) {
         // sample groups: the colour waits in the (now free) ray slot for the group's ordered sum
         *R.o[0] = scol.x; *R.o[1] = scol.y; *R.o[2] = scol.z;
         state = ST_PARKED;
@@ -1829,11 +1831,11 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
     // in sample order (the reference's (si, sj) order, mytracer_gpu.cu:202-221: sample s = si n + sj,
     // and a group holds samples chunk * G .. chunk * G + G - 1 on its lanes in order), then the group
     // starts its next chunk, or the pixel is stored and the group fetches another
-    if (P.group_log) {
+    if (group_log) {
       const unsigned long long full = full_groups(wballot(state == ST_PARKED));
       if (full != 0ull) {
         wave_lds_sync();   // the group's colours, written by its lanes in SHADE, are in LDS
-        const int gl = P.group_log;
+        const int gl = group_log;
         const int gbase = lane & ~((1 << gl) - 1);
         const bool group_done = ((full >> gbase) & 1ull) != 0ull;
         if (group_done && lane == gbase) {
@@ -2146,7 +2148,8 @@ struct Variant {
 // [0] production (4-wide), [1] 4-wide + counters, [2] canonical 2-wide counters
 // (the traversal the oracle replicates: tests pin its node / triangle counts),
 // [3] production + per-round timeline (RT_FLAG_TIMELINE, diagnostics), [4] production with a
-// 16-entry stack ring (deep hierarchies).  (A suspend/resume variant for deep scenes' several-frame
+// 16-entry stack ring (deep hierarchies), [5] / [6] = [0] / [4] with sample groups (spp > 1, DESIGN.md
+// §11.6; separate instances, so the one-sample kernels carry none of the group code).  (A suspend/resume variant for deep scenes' several-frame
 // launches, rounds 3-4, was removed in round 5: +0.2 % on config 4 against 21-30 MB per frame of
 // parked-state writes)
 const Variant kVariants[] = {
@@ -2155,12 +2158,14 @@ const Variant kVariants[] = {
     {render_kernel<2, true>, true},
     {render_kernel<4, false, true>, false},
     {render_kernel<4, false, false, 16>, false},
+    {render_kernel<4, false, false, kShortStack, true>, false},
+    {render_kernel<4, false, false, 16, true>, false},
 };
-constexpr int kNumVariants = 5;
+constexpr int kNumVariants = 7;
 // rt_upload_options.spp_lanes = 0: sample groups for spp > 1 launches or not
-constexpr bool kSppLanesDefault = false;
+constexpr bool kSppLanesDefault = true;   // config 3 +22.6 %, config 5 +19.3 % (r06d)
 constexpr int kRingDeep = 16;
-inline int variant_ring(int v) { return v == 4 ? kRingDeep : kShortStack; }
+inline int variant_ring(int v) { return (v == 4 || v == 6) ? kRingDeep : kShortStack; }
 // LDS per block: the variant's stack ring (ring entries per thread, at address 0: the kernel's
 // slot offsets are compile-time constants), kSlotDoubles doubles of slot, task + visibility words.
 size_t lds_bytes(int /*stack_words*/, int ring = kShortStack) {
@@ -2768,7 +2773,7 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   // costs, so launches that record or use them keep one lane per pixel
   const bool group = !list && !cost_debug && P.nsamp > 1 && (P.nsamp & (P.nsamp - 1)) == 0 &&
                      (sc->spp_lanes > 0 || (sc->spp_lanes == 0 && kSppLanesDefault)) &&
-                     !(p->flags & RT_FLAG_COST_ORDER);
+                     !(p->flags & (RT_FLAG_COST_ORDER | RT_FLAG_TRAVERSAL_STATS | RT_FLAG_WIDE_STATS | RT_FLAG_TIMELINE));
   if (group) {
     P.group_log = 0;
     while ((1 << (P.group_log + 1)) <= std::min(P.nsamp, 64)) P.group_log++;
@@ -2833,8 +2838,8 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   const int v = (p->flags & RT_FLAG_TRAVERSAL_STATS) ? 2
                 : (p->flags & RT_FLAG_WIDE_STATS) ? 1
                 : (p->flags & RT_FLAG_TIMELINE) ? 3
-                : sc->deep ? 4   // the 16-entry-ring production variant
-                : 0;
+                : sc->deep ? (group ? 6 : 4)   // the 16-entry-ring production variant
+                : group ? 5 : 0;
   const int ring = variant_ring(v);
   const int n_top = sc->n_top_v[v];
   const size_t lds = lds_bytes_total(sc->stack_words, n_top, ring);

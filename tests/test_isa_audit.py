@@ -23,7 +23,8 @@ import waitcnt_audit  # noqa: E402
 # the production kernels (no scratch): the static walk of the diagnostic variants, which spill 50-250
 # VGPRs to scratch, reaches spill reloads through infeasible exec-mask paths (reports that the
 # branch-insensitive walk cannot rule out), so the load-wait audit covers the shipped variants
-WAIT_VARIANTS = ["ILi4ELb0ELb0ELi8EE", "ILi4ELb0ELb0ELi16EE"]
+# (one-sample and sample-group instances of both stack rings)
+WAIT_VARIANTS = ["ILi4ELb0ELb0ELi8ELb0EE", "ILi4ELb0ELb0ELi16ELb0EE", "ILi4ELb0ELb0ELi8ELb1EE", "ILi4ELb0ELb0ELi16ELb1EE"]
 
 
 @pytest.fixture(scope="module")
