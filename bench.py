@@ -937,11 +937,11 @@ def workload_label(a, n_tris):
 
 def default_frames(a):
     """Frames per launch when --frames is not given: about 2.6e8 samples per launch (a power of
-    two, 1..128).  One frame of many samples is already a long launch with a negligible drain,
-    and batching such frames costs coherence: a lane keeps its pixel through all n*n samples, and
-    with several frames per launch the waves' lanes drift apart (4K 4x4 spp: SIMD efficiency of
-    the node loop 0.88 at 1 frame, 0.76 at 16; 24.3 ms per frame at 2 frames per launch, 28.4 at
-    16; tools/batch_probe.py, tools/batch_diag.py).  At 1 spp more frames only help."""
+    two, 1..128).  One frame of many samples is already a long launch with a negligible drain.
+    (Measured in round 3 with one lane per pixel, its n*n samples in sequence: batching such frames
+    cost coherence, the waves' lanes drifting apart -- 4K 4x4 spp 24.3 ms per frame at 2 frames per
+    launch, 28.4 at 16; HISTORY §4.  Round 6's sample groups keep a pixel's samples on neighbouring
+    lanes)  At 1 spp more frames only help."""
     samples = a.width * a.height * a.spp * a.spp
     return int(min(128, max(1, 2 ** round(math.log2(max(1.0, 2.6e8 / samples))))))
 

@@ -585,7 +585,7 @@ constexpr int kWavesPerEU = RT_WAVES_PER_EU;
 // [n h / 8, n (h + 1) / 8) is reordered so its expensive tiles come first, by the cost its tile
 // position had in the previous ordered launch (pixel lifetimes, 10-ns ticks).  A one-frame
 // launch's drain -- waves finishing the paths they started just before the queue ran dry -- is
-// then made of cheap tiles (office 1080p: kernel -11 %, tools/order_probe.py; DESIGN.md §4
+// then made of cheap tiles (office 1080p: kernel -11 %, HISTORY.md §4; DESIGN.md §4
 // "cost-ordered tiles").  The order is built inside the render kernel by its first blocks to run
 // out of work, from the cost map of the launch before, so it costs no launch and no busy CU.
 constexpr int kOrderItems = 16;
@@ -1165,12 +1165,10 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
       // only inside that loop, so it stays wave-uniform (an SGPR: the check costs SALU only).
       // A loop that runs past kTravGuard iterations abandons the ray (results void) and flags
       // the launch.  (Cost: 0.3 % for the node loop, A/B.)
-      // (the wave then ends, below: a corrupt hierarchy costs each wave one guard's worth of
-      // iterations, not one per ray)
-      bool tripped = false;
+      // (the ray is abandoned; a corrupt hierarchy costs each traversal that enters it one guard's
+      // worth of iterations -- a per-wave exit flag measured -1.4 % on the office, r06e)
       auto guard_trip = [&]() {
         if (lane == __ffsll((long long)wballot(1)) - 1) trip_watchdog(P.ctr, P.guard_host);
-        tripped = true;
       };
       // tests the triangles of leaf `lref` in record order; true = any-hit ray occluded
       auto test_leaf = [&](uint32_t lref) -> bool {
@@ -1439,9 +1437,6 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
         }
       }
       thit = tlim;
-      // a watchdog fired in this traversal: the persistent loop's check ends the wave next time
-      // (wave-uniform here, so the loop counter stays scalar)
-      if (wballot(tripped) != 0ull) guard = kGuardIters;
     }
     asm volatile("" ::: "memory");
     if (STATS) { const unsigned long long t = stamp(); d_trav += t - t_stamp; t_stamp = t; }
@@ -2574,7 +2569,7 @@ int read_counters(const LaunchCtx& C, unsigned long long* c) {
 // The CU-masked stream a launch from caller stream `caller` runs on (reserve_cus > 0): the mask
 // clears the first reserve_cus CU bits, so a concurrent kernel -- an RCCL gather whose waves need
 // 256 VGPRs, more than any single free block slot of the persistent grid offers -- finds whole CUs
-// free.  Measured with a kernel of RCCL's resource shape (tools/cumask_probe.py,
+// free.  Measured with a kernel of RCCL's resource shape (git 1a5bb03:tools/cumask_probe.py,
 // profiles/r04/r04e_cumask.txt): it runs beside the grid only when the first 32 bits are clear
 // (one XCD's worth); 8 or 16 CUs, or 32 spread over the mask, leave it waiting for the grid's end
 // (DESIGN.md §8).
