@@ -744,7 +744,8 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
   auto ST_SCOL_W = [&](D3 scol, double w) { ST4(R_SCOLW, scol, w); };
 
   // wave-uniform work-head cursor; in list mode the work count comes from the device
-  const long long n_list = P.list ? (long long)*P.list_count * P.nsamp : 0;   // work items
+  // work items of the list mode: one per (listed pixel, sample), or per listed pixel with sample groups
+  const long long n_list = P.list ? (long long)*P.list_count * (group_log ? 1 : P.nsamp) : 0;
   const long long n_tiles = P.list ? (n_list + 63) / 64 : P.n_tiles;
   int head = blockIdx.x % kGroups;
   int heads_left = kGroups;
@@ -940,7 +941,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
           if (P.list) {   // adaptive pass: one sample of a listed pixel
             // (the divisors made opaque here: the compiler would otherwise keep their reciprocals in
             // registers across the whole persistent loop)
-            long long ns = P.nsamp;
+            long long ns = group_log ? 1 : P.nsamp;   // sample groups: one work item per listed pixel
             uint32_t wd = (uint32_t)P.W;
             asm volatile("" : "+s"(ns), "+s"(wd));
             const uint32_t id = wk < n_list ? P.list[wk / ns] : 0xffffffffu;
@@ -968,7 +969,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
             py = (P.stripe_count == 1)
                      ? P.row_begin + lrow
                      : stripe_row(P, lrow);
-            if (P.list) {
+            if (P.list && !group_log) {
               long long ns = P.nsamp;
               asm volatile("" : "+s"(ns));
               sample = (int)(item % ns);
@@ -1775,15 +1776,15 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
           }
         }
       }
-      if (finish && P.list) {   // adaptive pass: this sample's trace() colour
+      if (finish && group_log) {
+        // sample groups: the colour waits in the (now free) ray slot for the group's ordered sum
+        *R.o[0] = scol.x; *R.o[1] = scol.y; *R.o[2] = scol.z;
+        state = ST_PARKED;
+      } else if (finish && P.list) {   // adaptive pass: this sample's trace() colour
         const D3 c = scol;
         double* so = P.sample_out + 3 * (size_t)item;
         so[0] = c.x; so[1] = c.y; so[2] = c.z;
         state = heads_left > 0 ? ST_FETCH : ST_DONE;
-      } else if (finish && group_log) {
-        // sample groups: the colour waits in the (now free) ray slot for the group's ordered sum
-        *R.o[0] = scol.x; *R.o[1] = scol.y; *R.o[2] = scol.z;
-        state = ST_PARKED;
       } else if (finish) {
         if (P.tile_cost) {   // cost of this sample: its bounces, or in time mode the pixel's lifetime at its
                              // last sample, summed per tile position over the launch's frames
@@ -2628,6 +2629,16 @@ static bool guard_tripped(const rt_scene* sc) {
   return sc->h_guard && *reinterpret_cast<const volatile unsigned int*>(sc->h_guard) != 0u;
 }
 
+// Sample groups for this launch (spp > 1, n^2 a power of two, rt_upload_options.spp_lanes): a pixel's
+// samples on neighbouring lanes, summed in order on chip.  The tile-cost maps record per-lane pixel
+// costs and the diagnostic variants have no group instance, so those launches keep one lane per pixel.
+bool use_groups(const rt_scene* sc, const rt_render_params* p) {
+  const int nsamp = p->spp_n * p->spp_n;
+  return nsamp > 1 && (nsamp & (nsamp - 1)) == 0 && (sc->spp_lanes > 0 || (sc->spp_lanes == 0 && kSppLanesDefault)) &&
+         !(p->flags & (RT_FLAG_COST_ORDER | RT_FLAG_TRAVERSAL_STATS | RT_FLAG_WIDE_STATS | RT_FLAG_TIMELINE |
+                       RT_FLAG_TILE_COST | RT_FLAG_TILE_COST_TIME));
+}
+
 int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* const* outs, rt_stats* stats,
                   void* stream, const uint32_t* list, const unsigned long long* count, long long list_cap,
                   double* sample_out = nullptr) {
@@ -2736,7 +2747,16 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   if (P.out_global && list) return fail(RT_ERR_INVALID, "RT_FLAG_GLOBAL_ROWS is not supported by the adaptive pass");
   P.tiles_x = (P.W + kTileW - 1) / kTileW;
   P.nsamp = p->spp_n * p->spp_n;
-  P.frame_tiles = list ? (list_cap * P.nsamp + 63) / 64 : (long long)P.tiles_x * ((rows + kTileH - 1) / kTileH);
+  // sample groups (spp > 1): a pixel's samples on G = min(n^2, 64) neighbouring lanes (use_groups);
+  // in list mode (the adaptive pass) the caller chose it: no sample buffer
+  const bool group = list ? sample_out == nullptr : use_groups(sc, p);
+  if (group) {
+    P.group_log = 0;
+    while ((1 << (P.group_log + 1)) <= std::min(P.nsamp, 64)) P.group_log++;
+    P.chunks = P.nsamp >> P.group_log;
+  }
+  P.frame_tiles = list ? (list_cap * (group ? 1 : P.nsamp) + 63) / 64
+                       : (long long)P.tiles_x * ((rows + kTileH - 1) / kTileH);
   P.n_tiles = P.frame_tiles * n_frames;
   if (P.n_tiles >= (1LL << 31)) return fail(RT_ERR_INVALID, "rt_launch: more than 2^31 tiles in one launch");
   P.div_row_tiles = div_magic((uint32_t)P.tiles_x * (uint32_t)n_frames);
@@ -2763,17 +2783,6 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
                     RT_FLAG_TILE_COST_TIME | RT_FLAG_NATURAL_ORDER)) &&
       !debug_order && (!sc->maps_used || sc->maps_stream == st);
   const bool cost_debug = !list && (p->flags & (RT_FLAG_TILE_COST | RT_FLAG_TILE_COST_TIME));
-  // sample groups (spp > 1): a pixel's samples on G = min(n^2, 64) neighbouring lanes, n^2 a power of
-  // two (groups tile the wave), summed in order on chip; the tile-cost maps record per-lane pixel
-  // costs, so launches that record or use them keep one lane per pixel
-  const bool group = !list && !cost_debug && P.nsamp > 1 && (P.nsamp & (P.nsamp - 1)) == 0 &&
-                     (sc->spp_lanes > 0 || (sc->spp_lanes == 0 && kSppLanesDefault)) &&
-                     !(p->flags & (RT_FLAG_COST_ORDER | RT_FLAG_TRAVERSAL_STATS | RT_FLAG_WIDE_STATS | RT_FLAG_TIMELINE));
-  if (group) {
-    P.group_log = 0;
-    while ((1 << (P.group_log + 1)) <= std::min(P.nsamp, 64)) P.group_log++;
-    P.chunks = P.nsamp >> P.group_log;
-  }
   const bool cost_order = !list && !group && n_frames == 1 && ((p->flags & RT_FLAG_COST_ORDER) || implicit_order);
   if (cost_order || cost_debug) {
     const long long n_pos = (long long)P.tiles_x * ((rows + kTileH - 1) / kTileH);
@@ -3026,10 +3035,15 @@ int rt_launch_adaptive_shard(rt_scene* sc, const rt_render_params* p, const doub
   // interior pixels only can be selected
   const long long cap = (long long)std::max(0, W - 2) * G.rows;
   const int nsamp = subp * subp;
+  rt_render_params q = *p;
+  q.spp_n = subp;
+  // sample groups: a selected pixel's subp^2 samples on neighbouring lanes, summed in order and stored
+  // by the render kernel itself -- no sample buffer, no reduce kernel
+  const bool grp = use_groups(sc, &q);
   StreamScratch scratch{st, {}};
   HIP_TRY(scratch.alloc(&list, (size_t)std::max(1LL, cap) * sizeof(uint32_t)));
   HIP_TRY(scratch.alloc(&cnt, sizeof(unsigned long long)));
-  HIP_TRY(scratch.alloc(&samples, (size_t)std::max(1LL, cap) * nsamp * 3 * sizeof(double)));
+  if (!grp) HIP_TRY(scratch.alloc(&samples, (size_t)std::max(1LL, cap) * nsamp * 3 * sizeof(double)));
   HIP_TRY(hipMemsetAsync(cnt, 0, sizeof(unsigned long long), st));
   const int tiles_x = (W + 7) / 8;
   const long long n_tiles = (long long)tiles_x * ((G.rows + 7) / 8);
@@ -3039,10 +3053,8 @@ int rt_launch_adaptive_shard(rt_scene* sc, const rt_render_params* p, const doub
                        d_halo, d_out, p->out_format, G, threshold, tiles_x, n_tiles, list, cnt, 0u, nullptr, nullptr);
     HIP_TRY(hipGetLastError());
   }
-  rt_render_params q = *p;
-  q.spp_n = subp;
   int rc = launch_render(sc, &q, 1, &d_out, stats, stream, list, cnt, cap, samples);
-  if (rc == RT_OK && cap > 0) {
+  if (rc == RT_OK && cap > 0 && !grp) {
     hipLaunchKernelGGL(adaptive_reduce_kernel, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, st, list, cnt,
                        samples, nsamp, d_out, p->out_format, nullptr);
     HIP_TRY(hipGetLastError());
@@ -3111,18 +3123,27 @@ int rt_launch_adaptive_frames(rt_scene* sc, const rt_render_params* p, int n_fra
                        n_tiles, list, cnt, 0u, reinterpret_cast<const double* const*>(d_ptrs), d_ptrs + n_frames);
     HIP_TRY(hipGetLastError());
   }
-  // every sample of every selected pixel of every frame in one launch: the sample buffer is sized
-  // by the selection count (read back: one synchronisation per batch)
-  unsigned long long n_sel = 0;
-  HIP_TRY(hipMemcpyAsync(&n_sel, cnt, sizeof n_sel, hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
-  const int nsamp = subp * subp;
-  double* samples = nullptr;
-  HIP_TRY(scratch.alloc(&samples, (size_t)std::max(1ull, n_sel) * nsamp * 3 * sizeof(double)));
+  // every sample of every selected pixel of every frame in one launch.  Sample groups (use_groups):
+  // the render kernel sums and stores each pixel itself, its work count read on the device -- nothing
+  // to size, no host synchronisation; otherwise the sample buffer is sized by the selection count
+  // (read back: one synchronisation per batch) and a reduce kernel sums it
   std::vector<rt_render_params> q(p, p + n_frames);
   for (auto& x : q) x.spp_n = subp;
-  int rc = launch_render(sc, q.data(), n_frames, d_out, stats, stream, list, cnt, (long long)n_sel, samples);
-  if (rc == RT_OK && n_sel > 0) {   // sums in (si, sj) order into each frame's output (this call's table)
+  const bool grp = use_groups(sc, &q[0]);
+  const int nsamp = subp * subp;
+  unsigned long long n_sel = 0;
+  double* samples = nullptr;
+  if (!grp) {
+    HIP_TRY(hipMemcpyAsync(&n_sel, cnt, sizeof n_sel, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(scratch.alloc(&samples, (size_t)std::max(1ull, n_sel) * nsamp * 3 * sizeof(double)));
+  }
+  int rc = launch_render(sc, q.data(), n_frames, d_out, stats, stream, list, cnt, grp ? cap : (long long)n_sel, samples);
+  if (rc == RT_OK && grp && n_selected) {
+    HIP_TRY(hipMemcpyAsync(&n_sel, cnt, sizeof n_sel, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+  }
+  if (rc == RT_OK && !grp && n_sel > 0) {   // sums in (si, sj) order into each frame's output (this call's table)
     hipLaunchKernelGGL(adaptive_reduce_kernel, dim3((unsigned)((n_sel + 255) / 256)), dim3(256), 0, st, list, cnt,
                        samples, nsamp, nullptr, p->out_format, d_ptrs + n_frames);
     HIP_TRY(hipGetLastError());

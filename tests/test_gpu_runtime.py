@@ -232,3 +232,42 @@ def test_sample_groups_equal_lane_per_pixel(office, n):
         st_off.primary_rays + st_off.shadow_rays + st_off.reflection_rays
     on.close()
     off.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("subp", [2, 3, 4, 8, 16])
+def test_adaptive_sample_groups_equal_sample_buffer(office, subp):
+    # The adaptive pass with sample groups (a selected pixel's subp^2 samples on neighbouring lanes,
+    # summed in (si, sj) order by the render kernel: no sample buffer, no reduce kernel, no
+    # read-back of the selection count) against the sample-buffer path (spp_lanes = -1): the same
+    # pixels bit for bit, the same selection and ray counts -- one frame, several frames in one
+    # launch, a row shard with its halo, every interior pixel selected (threshold -1).
+    import torch
+
+    hs, _ = office
+    on, off = rtamd.DeviceScene(hs, 0, spp_lanes=1), rtamd.DeviceScene(hs, 0, spp_lanes=-1)
+    w, h = (64, 40) if subp <= 8 else (24, 16)
+    p = hs.render_params(w, h, 1)
+    p.out_format = rtamd.RT_OUT_RGB_F64
+    rays = lambda s: (s.primary_rays, s.shadow_rays, s.reflection_rays)  # noqa: E731
+    cams = [rtamd.camera_orbit(p, 0.05 * f) for f in range(3)]
+    prims = [torch.zeros((h, w, 3), dtype=torch.float64, device="cuda") for _ in cams]
+    on.launch_frames(cams, [x.data_ptr() for x in prims])
+    for thr in (0.02, -1.0):
+        res = {}
+        for k, d in (("on", on), ("off", off)):
+            outs = [torch.full((h, w, 3), float("nan"), dtype=torch.float64, device="cuda") for _ in cams]
+            one = torch.full((h, w, 3), float("nan"), dtype=torch.float64, device="cuda")
+            s1, n1 = d.launch_adaptive(cams[1], prims[1].data_ptr(), one.data_ptr(), subp, thr, stats=True)
+            sf, nf = d.launch_adaptive_frames(cams, [x.data_ptr() for x in prims], [o.data_ptr() for o in outs],
+                                              subp, thr, stats=True)
+            torch.cuda.synchronize()
+            res[k] = (one.cpu().numpy(), rays(s1), n1, [o.cpu().numpy() for o in outs], rays(sf), nf)
+        a, b = res["on"], res["off"]
+        assert a[2] == b[2] and a[5] == b[5] and a[2] > 0
+        assert a[1] == b[1] and a[4] == b[4]
+        assert np.array_equal(a[0], b[0], equal_nan=True)
+        for x, y in zip(a[3], b[3]):
+            assert np.array_equal(x, y, equal_nan=True)
+    on.close()
+    off.close()

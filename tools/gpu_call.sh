@@ -8,7 +8,8 @@ export TMPDIR=/tmp
 TAG=${1:?tag}; PT=$2; shift 2
 mkdir -p gpurun_out
 if [ -n "$PT" ]; then
-  timeout -k 10 720 python -u -m pytest -v --timeout 200 --timeout-method thread $PT > gpurun_out/${TAG}_gpu_tests.txt 2>&1
+  # (PT is shell words: -k "a or b" keeps its quotes)
+  eval "timeout -k 10 720 python -u -m pytest -v --timeout 200 --timeout-method thread $PT" > gpurun_out/${TAG}_gpu_tests.txt 2>&1
   rc=$?
   tail -3 gpurun_out/${TAG}_gpu_tests.txt
   if [ $rc -ge 124 ] || [ $rc -eq 2 ] || [ $rc -gt 5 ]; then echo "tests ended with $rc: stopping"; exit $rc; fi
