@@ -249,7 +249,8 @@ typedef struct rt_upload_options {
                             order on chip), -1 = one lane per pixel, its samples in sequence; 0 = the default,
                             groups (4K 16 spp +22.6 %, 8K 64 spp +19.3 %).  Launches with
                             other n, the diagnostic flags, tile-cost maps or RT_FLAG_COST_ORDER keep one lane
-                            per pixel.  Pixels and ray counts are identical either way */
+                            per pixel.  The adaptive pass follows it too (groups: no sample buffer, no
+                            reduce kernel).  Pixels and ray counts are identical either way */
   int reserved_[5];
 } rt_upload_options;
 
@@ -329,10 +330,12 @@ int rt_launch_adaptive(rt_scene* scene, const rt_render_params* p, const double*
  * p[0..n_frames) differ only in their camera vectors (as rt_launch_frames), d_primary[f] is frame
  * f's fp64 primary image, d_out[f] its output.  Every frame's selection goes into one list and
  * one launch traces every sample of every selected pixel of every frame (a pixel's samples on
- * neighbouring lanes, as rt_launch_adaptive), so the per-launch drain is paid once per batch;
- * the sample buffer is sized by the selection count, which the call reads back (one host
- * synchronisation per call).  Results equal rt_launch_adaptive on each frame.  W x H < 2^25.
- * *n_selected (optional) = pixels re-rendered over all frames. */
+ * neighbouring lanes, as rt_launch_adaptive), so the per-launch drain is paid once per batch.
+ * subp^2 a power of two (sample groups, rt_upload_options.spp_lanes >= 0): the render kernel sums
+ * and stores each selected pixel itself and the call does not synchronise; otherwise a sample
+ * buffer sized by the selection count, which the call reads back (one host synchronisation per
+ * call), and a reduce kernel.  Results equal rt_launch_adaptive on each frame.  W x H < 2^25.
+ * *n_selected (optional, synchronising) = pixels re-rendered over all frames. */
 int rt_launch_adaptive_frames(rt_scene* scene, const rt_render_params* p, int n_frames, const double* const* d_primary,
                               void* const* d_out, int subp, double threshold, rt_stats* stats, long long* n_selected,
                               void* stream);
