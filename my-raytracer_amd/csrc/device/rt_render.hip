@@ -2757,7 +2757,8 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   }
   P.frame_tiles = list ? (list_cap * (group ? 1 : P.nsamp) + 63) / 64
                        : (long long)P.tiles_x * ((rows + kTileH - 1) / kTileH);
-  P.n_tiles = P.frame_tiles * n_frames;
+  // (list mode: one list holds every frame's items, list_cap counts them all)
+  P.n_tiles = list ? P.frame_tiles : P.frame_tiles * n_frames;
   if (P.n_tiles >= (1LL << 31)) return fail(RT_ERR_INVALID, "rt_launch: more than 2^31 tiles in one launch");
   P.div_row_tiles = div_magic((uint32_t)P.tiles_x * (uint32_t)n_frames);
   P.div_tiles_x = div_magic((uint32_t)P.tiles_x);

@@ -1,7 +1,8 @@
 """Extended parity sweep (dev tool, under gpurun): the GPU suite's seeded random scenes
 (tests/fuzz_scenes.py) over many more seeds than the suite runs, each rendered by the production
 kernel and by the CPU oracle (reference CPU semantics, oracle/) and compared -- fp64 pixels within
-1e-12, ray counts exact.  Per seed: the plain mesh scene at an odd image size with 1-3 spp, the
+1e-12, ray counts exact.  Per seed, at an odd image size with n x n spp, n = 1-4 (n = 2, 4:
+sample groups, the default since round 6; n = 3: one lane per pixel): the plain mesh scene, the
 same scene with spheres and planes (analytic path, CPU intersect_scene semantics) and with a
 textured mesh; every 5th seed also on the SAH and refined-reference device trees (bit-identical
 to the default SBVH).  The oracle here is the checker, never the thing measured.
@@ -91,7 +92,7 @@ def main():
         tmp = Path(td)
         for seed in range(s0, s0 + n):
             w, h = 33 + seed % 40, 21 + (seed * 7) % 31        # odd and even sizes, partial tiles
-            spp = 1 + seed % 3
+            spp = 1 + seed % 4
             trees = ("sbvh", "sah", "reference") if seed % 5 == 0 else ("sbvh",)
             res = {"seed": seed, "size": [w, h], "spp": spp}
             for kind, writer, analytic in (("mesh", fuzz_scenes.write, False),
@@ -101,7 +102,7 @@ def main():
                 d.mkdir()
                 hs = rtamd.HostScene.load(writer(d, seed, w, h))
                 hs.prepare()
-                p = hs.render_params(0, 0, spp if kind == "mesh" else 1)
+                p = hs.render_params(0, 0, spp)
                 err, same, rays = check(hs, p, analytic, trees if kind == "mesh" else ("sbvh",))
                 ok = err <= TOL64 and same
                 res[kind] = {"max_abs_err": err, "exact_counts_and_trees": same, "rays": rays, "ok": ok}
