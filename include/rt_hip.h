@@ -246,7 +246,9 @@ typedef struct rt_upload_options {
                             default), -1 = exact */
   int spp_lanes;         /* n x n > 1 samples per pixel, n^2 a power of two: 1 = a pixel's samples on
                             neighbouring lanes of one wave (groups of G = min(n^2, 64) lanes, summed in sample
-                            order on chip), -1 = one lane per pixel, its samples in sequence; 0 = the default,
+                            order on chip), 2..64 (a power of two) = the same with G capped at that many
+                            lanes (chunks of G samples in sequence), -1 = one lane per pixel, its samples in
+                            sequence; 0 = the default,
                             groups (4K 16 spp +22.6 %, 8K 64 spp +19.3 %).  Launches with
                             other n, the diagnostic flags, tile-cost maps or RT_FLAG_COST_ORDER keep one lane
                             per pixel.  The adaptive pass follows it too (groups: no sample buffer, no

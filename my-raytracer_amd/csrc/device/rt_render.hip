@@ -2445,7 +2445,8 @@ int resolve_options(const rt_upload_options* opt, rt_upload_options& o) {
   if (o.reserve_cus < -1) return fail(RT_ERR_INVALID, "rt_scene_upload: reserve_cus must be >= -1");
   if (o.order_window < -1 || o.order_window > 64)
     return fail(RT_ERR_INVALID, "rt_scene_upload: order_window must be in [-1, 64]");
-  if (o.spp_lanes < -1 || o.spp_lanes > 1) return fail(RT_ERR_INVALID, "rt_scene_upload: spp_lanes must be -1, 0 or 1");
+  if (o.spp_lanes < -1 || o.spp_lanes > 64 || (o.spp_lanes > 1 && (o.spp_lanes & (o.spp_lanes - 1)) != 0))
+    return fail(RT_ERR_INVALID, "rt_scene_upload: spp_lanes must be -1, 0, 1 or a power of two <= 64");
   if (o.stack_ring != 0 && o.stack_ring != 8 && o.stack_ring != 16)
     return fail(RT_ERR_INVALID, "rt_scene_upload: stack_ring must be 0, 8 or 16");
   if (o.blocks_per_cu < 0 || o.grid_spare < 0 || o.build_threads < 0)
@@ -2752,7 +2753,10 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   const bool group = list ? sample_out == nullptr : use_groups(sc, p);
   if (group) {
     P.group_log = 0;
-    while ((1 << (P.group_log + 1)) <= std::min(P.nsamp, 64)) P.group_log++;
+    // G = min(n^2, 64), or the group-size cap spp_lanes >= 2 (chunks of G samples, the running sum
+    // in the path state between them)
+    const int gmax = sc->spp_lanes >= 2 ? sc->spp_lanes : 64;
+    while ((1 << (P.group_log + 1)) <= std::min(P.nsamp, gmax)) P.group_log++;
     P.chunks = P.nsamp >> P.group_log;
   }
   P.frame_tiles = list ? (list_cap * (group ? 1 : P.nsamp) + 63) / 64

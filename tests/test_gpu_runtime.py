@@ -235,6 +235,38 @@ def test_sample_groups_equal_lane_per_pixel(office, n):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n,cap", [(4, 4), (8, 16), (8, 2), (16, 32)])
+def test_sample_group_size_cap_changes_no_pixel(office, n, cap):
+    # rt_upload_options.spp_lanes = 2..64 caps the group at that many lanes: the n^2 samples then
+    # run in n^2 / cap chunks (the running sum in the path state between chunks), in sample order
+    import torch
+
+    hs, _ = office
+    capd, off = rtamd.DeviceScene(hs, 0, spp_lanes=cap), rtamd.DeviceScene(hs, 0, spp_lanes=-1)
+    w, h = (48, 32) if n <= 8 else (20, 12)
+    p = hs.render_params(w, h, n)
+    p.out_format = rtamd.RT_OUT_RGB_F64
+    a, sa = capd.render(p)
+    b, sb = off.render(p)
+    assert np.array_equal(a, b)
+    assert [sa.primary_rays, sa.shadow_rays, sa.reflection_rays] == [sb.primary_rays, sb.shadow_rays, sb.reflection_rays]
+    p1 = hs.render_params(w, h, 1)
+    p1.out_format = rtamd.RT_OUT_RGB_F64
+    prim = torch.zeros((h, w, 3), dtype=torch.float64, device="cuda")
+    capd.launch(p1, prim.data_ptr())
+    outs = [torch.full((h, w, 3), float("nan"), dtype=torch.float64, device="cuda") for _ in range(2)]
+    _, n1 = capd.launch_adaptive(p1, prim.data_ptr(), outs[0].data_ptr(), n, -1.0, stats=True)
+    _, n2 = off.launch_adaptive(p1, prim.data_ptr(), outs[1].data_ptr(), n, -1.0, stats=True)
+    torch.cuda.synchronize()
+    assert n1 == n2 and torch.equal(outs[0], outs[1])
+    capd.close()
+    off.close()
+    for bad in (-2, 3, 6, 128):   # -1, 0, 1 or a power of two <= 64
+        with pytest.raises(RuntimeError):
+            rtamd.DeviceScene(hs, 0, spp_lanes=bad)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("subp", [2, 3, 4, 8, 16])
 def test_adaptive_sample_groups_equal_sample_buffer(office, subp):
     # The adaptive pass with sample groups (a selected pixel's subp^2 samples on neighbouring lanes,
