@@ -245,7 +245,7 @@ typedef struct rt_upload_options {
                             exact costs for hierarchies from 2^18 device records on, whatever stack_ring forces;
                             default), -1 = exact */
   int spp_lanes;         /* n x n > 1 samples per pixel, n^2 a power of two: 1 = a pixel's samples on
-                            neighbouring lanes of one wave (groups of G = min(n^2, 64) lanes, summed in sample
+                            neighbouring lanes of one wave (groups of G = min(n^2, 32) lanes, summed in sample
                             order on chip), 2..64 (a power of two) = the same with G capped at that many
                             lanes (chunks of G samples in sequence), -1 = one lane per pixel, its samples in
                             sequence; 0 = the default,

@@ -2160,6 +2160,9 @@ const Variant kVariants[] = {
 constexpr int kNumVariants = 7;
 // rt_upload_options.spp_lanes = 0: sample groups for spp > 1 launches or not
 constexpr bool kSppLanesDefault = true;   // config 3 +22.6 %, config 5 +19.3 % (r06d)
+// default group-size cap: 8K 64 spp at G = 32 (2 pixels per wave, 2 chunks each) +3.2 % over G = 64,
+// +0.7 % over G = 16; 4K 16 spp best at G = 16 = n^2 (r06o)
+constexpr int kGroupLanes = 32;
 constexpr int kRingDeep = 16;
 inline int variant_ring(int v) { return (v == 4 || v == 6) ? kRingDeep : kShortStack; }
 // LDS per block: the variant's stack ring (ring entries per thread, at address 0: the kernel's
@@ -2748,14 +2751,14 @@ int launch_render(rt_scene* sc, const rt_render_params* p, int n_frames, void* c
   if (P.out_global && list) return fail(RT_ERR_INVALID, "RT_FLAG_GLOBAL_ROWS is not supported by the adaptive pass");
   P.tiles_x = (P.W + kTileW - 1) / kTileW;
   P.nsamp = p->spp_n * p->spp_n;
-  // sample groups (spp > 1): a pixel's samples on G = min(n^2, 64) neighbouring lanes (use_groups);
+  // sample groups (spp > 1): a pixel's samples on G = min(n^2, 32) neighbouring lanes (use_groups);
   // in list mode (the adaptive pass) the caller chose it: no sample buffer
   const bool group = list ? sample_out == nullptr : use_groups(sc, p);
   if (group) {
     P.group_log = 0;
-    // G = min(n^2, 64), or the group-size cap spp_lanes >= 2 (chunks of G samples, the running sum
-    // in the path state between them)
-    const int gmax = sc->spp_lanes >= 2 ? sc->spp_lanes : 64;
+    // G = min(n^2, kGroupLanes), or the group-size cap spp_lanes >= 2 (chunks of G samples, the
+    // running sum in the path state between them)
+    const int gmax = sc->spp_lanes >= 2 ? sc->spp_lanes : kGroupLanes;
     while ((1 << (P.group_log + 1)) <= std::min(P.nsamp, gmax)) P.group_log++;
     P.chunks = P.nsamp >> P.group_log;
   }

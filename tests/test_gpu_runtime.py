@@ -197,7 +197,7 @@ def test_multi_calls_keep_the_current_device(office):
 @pytest.mark.parametrize("n", [2, 3, 4, 8, 16])
 def test_sample_groups_equal_lane_per_pixel(office, n):
     # spp_lanes = 1: a pixel's n x n samples run on neighbouring lanes of one wave (groups of
-    # min(n^2, 64) lanes; n^2 = 256: four chunks of 64 with the running sum in the path state) and are
+    # min(n^2, 32) lanes; n^2 = 64, 256: two / eight chunks of 32 with the running sum in the path state) and are
     # summed in sample order on chip; n = 3 (9 samples, not a power of two) keeps one lane per pixel.
     # Pixels and ray counts equal the lane-per-pixel render bit for bit -- one frame, several frames
     # in one launch, a striped shard -- and the oracle within the fp64 tolerance.
