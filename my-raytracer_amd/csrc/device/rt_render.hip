@@ -2303,7 +2303,8 @@ const char* rt_last_error(void) { return g_error.c_str(); }
 
 const char* rt_build_info(void) {
   return "librt_hip: gfx950 persistent flattened render kernel; variants {4-wide 8-entry stack ring, 4-wide 16-entry ring (>= 2^18 triangle records), "
-         "4-wide+stats, 2-wide canonical stats, 4-wide+round timeline}; fp32 4-wide nodes (128 B) with an LDS treelet, "
+         "4-wide+stats, 2-wide canonical stats, 4-wide+round timeline, sample groups (spp > 1) on both rings}; "
+         "fp32 4-wide nodes (128 B) with an LDS treelet, "
          "fp64 triangles/shading, LDS ray slots + stack ring (global spill), global path state, 8 XCD work heads";
 }
 
