@@ -361,6 +361,15 @@ int rt_launch_adaptive_shard(rt_scene* scene, const rt_render_params* p, const d
  * Returns the entry count (2 x segments); rows_out may be NULL to query it. */
 int rt_adaptive_halo_rows(const rt_render_params* p, int* rows_out, int cap);
 
+/* The reference's whole launch_compute_image_device (mytracer_gpu.cu:44-113) in one synchronous
+ * call: the primary pass (fp64, device scratch), the adaptive pass (subp, threshold: the reference
+ * uses 4 and 0.02) and the copy of the final image into host_out (H x W x 3 of p->out_format; a
+ * page-locked, device-mapped buffer is written directly).  Full frame only.  st_primary /
+ * st_adaptive / n_selected optional.  Results equal rt_launch_compute_image (fp64) +
+ * rt_launch_adaptive on device buffers. */
+int rt_render_adaptive_to_host(rt_scene* scene, const rt_render_params* p, int subp, double threshold, void* host_out,
+                               rt_stats* st_primary, rt_stats* st_adaptive, long long* n_selected);
+
 /* Renders into a HOST buffer, synchronously (the reference's call pattern: Raytracer::
  * compute_image_cuda copies every frame back, mytracer.cpp:123-159).  A page-locked, device-mapped
  * buffer (hipHostMalloc, hipHostRegister, torch pin_memory) is written by the kernel directly over

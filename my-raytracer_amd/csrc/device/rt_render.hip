@@ -3199,6 +3199,57 @@ int rt_render_to_host(rt_scene* sc, const rt_render_params* p, void* host_out, r
   return rc;
 }
 
+int rt_render_adaptive_to_host(rt_scene* sc, const rt_render_params* p, int subp, double threshold, void* host_out,
+                               rt_stats* st_primary, rt_stats* st_adaptive, long long* n_selected) {
+  if (!sc || !p || !host_out) return fail(RT_ERR_INVALID, "rt_render_adaptive_to_host: null argument");
+  if (p->flags & RT_FLAG_GLOBAL_ROWS)
+    return fail(RT_ERR_INVALID, "rt_render_adaptive_to_host: RT_FLAG_GLOBAL_ROWS is not supported");
+  const int W = p->camera.width, H = p->camera.height;
+  if (W <= 0 || H <= 0) return fail(RT_ERR_INVALID, "bad image size");
+  if (p->stripe_count > 1 || p->row_begin != 0 || (p->row_end > 0 && p->row_end != H))
+    return fail(RT_ERR_INVALID, "rt_render_adaptive_to_host: needs the full frame (neighbour test), no stripes/row range");
+  if (p->out_format != RT_OUT_RGB_F32 && p->out_format != RT_OUT_RGB_F64) return fail(RT_ERR_INVALID, "bad out_format");
+  HIP_TRY(hipSetDevice(sc->device));
+  const size_t elem = p->out_format == RT_OUT_RGB_F64 ? sizeof(double) : sizeof(float);
+  const size_t bytes = (size_t)H * W * 3 * elem;
+  // the primary pass in fp64 (the selection compares fp64 colours, mytracer_gpu.cu:66-81), into
+  // stream-ordered scratch on the null stream
+  StreamScratch scratch{nullptr, {}};
+  double* prim = nullptr;
+  HIP_TRY(scratch.alloc(&prim, (size_t)H * W * 3 * sizeof(double)));
+  rt_render_params q = *p;
+  q.out_format = RT_OUT_RGB_F64;
+  int rc = rt_launch_compute_image(sc, &q, prim, st_primary, nullptr);
+  if (rc != RT_OK) return rc;
+  // the adaptive pass (mytracer_gpu.cu:83-109) writes every pixel of the output: straight into a
+  // page-locked, device-mapped caller buffer, else into the scene's staging buffer and one copy
+  hipPointerAttribute_t at;
+  void* direct = nullptr;
+  if (hipPointerGetAttributes(&at, host_out) == hipSuccess && at.type == hipMemoryTypeHost) {
+    if (hipHostGetDevicePointer(&direct, host_out, 0) != hipSuccess) direct = nullptr;
+  }
+  (void)hipGetLastError();   // pageable memory: the queries above fail, which is not an error here
+  if (!direct && sc->host_stage_bytes < bytes) {
+    HIP_TRY(hipDeviceSynchronize());   // an earlier call's copy may still read the old buffer
+    if (sc->d_host_stage) HIP_TRY(hipFree(sc->d_host_stage));
+    sc->d_host_stage = nullptr;
+    sc->host_stage_bytes = 0;
+    HIP_TRY(hipMalloc(&sc->d_host_stage, bytes));
+    sc->host_stage_bytes = bytes;
+  }
+  rc = rt_launch_adaptive(sc, p, prim, direct ? direct : sc->d_host_stage, subp, threshold, st_adaptive, n_selected,
+                          nullptr);
+  if (rc != RT_OK) return rc;
+  if (!direct) {
+    const hipError_t e = hipMemcpy(host_out, sc->d_host_stage, bytes, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("hipMemcpy D2H: ") + hipGetErrorString(e));
+  } else {
+    HIP_TRY(hipStreamSynchronize(nullptr));
+  }
+  if (guard_tripped(sc)) return fail(RT_ERR_HIP, kGuardMsg);
+  return RT_OK;
+}
+
 int rt_debug_counters(rt_scene* sc, unsigned long long* out, int n) {
   if (!sc || !out || n <= 0) return fail(RT_ERR_INVALID, "rt_debug_counters: bad argument");
   HIP_TRY(hipSetDevice(sc->device));

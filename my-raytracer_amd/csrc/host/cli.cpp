@@ -7,10 +7,13 @@
 //
 //   rt_render --scene office|cornell|random_tris|spheres|path.sce
 //             [--width W --height H --spp N --max-depth D --tris N --seed S
-//              --detail K --device I --gpus N --assembly gather|peer --frames F --out image.ppm]
+//              --detail K --device I --gpus N --assembly gather|peer --frames F --adaptive
+//              --out image.ppm]
 // --gpus N renders each frame on GPUs 0..N-1 (row stripes + one RCCL gather, rt_multi.h; with
 // --assembly peer every GPU stores its rows straight into device 0's frame instead);
-// without it one device (--device) renders through rt_launch_compute_image.
+// without it one device (--device) renders through rt_render_to_host.  --adaptive (one device):
+// the primary pass followed by the adaptive supersampling pass (subp 4, threshold 0.02), as the
+// reference's launch_compute_image_device always runs them (mytracer_gpu.cu:44-113).
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -55,7 +58,7 @@ class Raytracer {
     return true;
   }
   // Raytracer::compute_image_cuda equivalent.
-  bool compute_image(int width, int height, int spp, int max_depth, int frames) {
+  bool compute_image(int width, int height, int spp, int max_depth, int frames, bool adaptive) {
     if (rt_host_render_params(host_, width, height, spp, &params_) != RT_OK) return error(rt_host_last_error());
     if (max_depth >= 0) params_.max_depth = max_depth;
     image_.assign(3 * (size_t)params_.camera.width * params_.camera.height, 0.f);
@@ -70,13 +73,26 @@ class Raytracer {
         if (f == 0)   // (peer stores are kept only if the driver's bit check of the first frame passed)
           std::printf("frame assembly in use: %s\n",
                       rt_multi_assembly(multi_) == RT_MULTI_PEER ? "peer stores" : "RCCL gather");
+      } else if (adaptive) {
+        rt_stats st1;
+        long long n_sel = 0;
+        const auto t0 = std::chrono::steady_clock::now();
+        if (rt_render_adaptive_to_host(gpu_, &params_, 4, 0.02, image_.data(), &st, &st1, &n_sel) != RT_OK)
+          return error(rt_last_error());
+        ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        std::printf("frame %d: adaptive pass re-rendered %lld pixels (rays P %lld S %lld R %lld)\n", f, n_sel,
+                    st1.primary_rays, st1.shadow_rays, st1.reflection_rays);
+        st.primary_rays += st1.primary_rays;
+        st.shadow_rays += st1.shadow_rays;
+        st.reflection_rays += st1.reflection_rays;
       } else {
         if (rt_render_to_host(gpu_, &params_, image_.data(), &st) != RT_OK) return error(rt_last_error());
         rt_last_kernel_ms(gpu_, &ms);
       }
       const long long rays = st.primary_rays + st.shadow_rays + st.reflection_rays;
-      std::printf("frame %d: %dx%d spp %d  kernel %.3f ms  rays %lld (P %lld S %lld R %lld)  %.1f Mrays/s\n", f,
-                  params_.camera.width, params_.camera.height, params_.spp_n * params_.spp_n, ms, rays,
+      std::printf("frame %d: %dx%d spp %d  %s %.3f ms  rays %lld (P %lld S %lld R %lld)  %.1f Mrays/s\n", f,
+                  params_.camera.width, params_.camera.height, params_.spp_n * params_.spp_n,
+                  adaptive ? "call (both passes + copy)" : "kernel", ms, rays,
                   st.primary_rays, st.shadow_rays, st.reflection_rays, rays / (ms * 1e3));
     }
     return true;
@@ -106,6 +122,7 @@ class Raytracer {
 int main(int argc, char** argv) {
   std::string scene = "office", out;
   int width = 0, height = 0, spp = 1, max_depth = -1, device = 0, frames = 1, gpus = 0;
+  bool adaptive = false;
   std::string assembly = "gather";
   rt_gen_params gp{};
   gp.max_depth = -1;
@@ -128,13 +145,21 @@ int main(int argc, char** argv) {
     else if (a == "--gpus") gpus = std::atoi(next());
     else if (a == "--assembly") assembly = next();
     else if (a == "--out") out = next();
+    else if (a == "--adaptive") adaptive = true;
+    else if (a == "--help" || a == "-h") {
+      std::printf("usage: rt_render [--scene office|cornell|random_tris|spheres|FILE.sce] [--width W] [--height H]\n"
+                  "                 [--spp N] [--max-depth D] [--tris N] [--seed S] [--detail K] [--device I]\n"
+                  "                 [--gpus N [--assembly gather|peer]] [--frames F] [--adaptive] [--out image.ppm]\n");
+      return 0;
+    }
     else { std::fprintf(stderr, "unknown option %s\n", a.c_str()); return 2; }
   }
   Raytracer rt;
   if (gpus < 0) { std::fprintf(stderr, "--gpus must be >= 1\n"); return 2; }
   if (assembly != "gather" && assembly != "peer") { std::fprintf(stderr, "--assembly must be gather or peer\n"); return 2; }
+  if (adaptive && gpus >= 1) { std::fprintf(stderr, "--adaptive renders on one device (no --gpus)\n"); return 2; }
   if (!rt.init(scene, gp, device, gpus, assembly == "peer")) return 1;
-  if (!rt.compute_image(width, height, spp, max_depth, frames)) return 1;
+  if (!rt.compute_image(width, height, spp, max_depth, frames, adaptive)) return 1;
   if (!out.empty() && !rt.write(out)) return 1;
   return 0;
 }

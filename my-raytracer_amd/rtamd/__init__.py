@@ -365,6 +365,22 @@ class DeviceScene:
         st1, nsel = self.launch_adaptive(params, prim.data_ptr(), out.data_ptr(), subp, threshold, stats=True)
         return out.cpu().numpy(), st0, st1, nsel
 
+    def render_adaptive_to_host(self, params, subp=4, threshold=0.02, out=None):
+        """rt_render_adaptive_to_host: primary + adaptive pass + copy in one synchronous call (the
+        reference's launch_compute_image_device); out: a host array [H, W, 3] of params.out_format
+        (numpy, or a pinned torch tensor's numpy view).  Returns (image, primary Stats, adaptive
+        Stats, n_selected)."""
+        H, W = params.camera.height, params.camera.width
+        dtype = np.float64 if params.out_format == RT_OUT_RGB_F64 else np.float32
+        img = np.zeros((H, W, 3), dtype=dtype) if out is None else out
+        if img.shape != (H, W, 3) or img.dtype != dtype or not img.flags["C_CONTIGUOUS"]:
+            raise ValueError("out must be a C-contiguous [H, W, 3] array of the output format")
+        st0, st1, nsel = abi.Stats(), abi.Stats(), C.c_longlong(-1)
+        _check_hip(hip_lib().rt_render_adaptive_to_host(self._h, C.byref(params), subp, threshold,
+                                                        img.ctypes.data_as(C.c_void_p), C.byref(st0), C.byref(st1),
+                                                        C.byref(nsel)), "rt_render_adaptive_to_host")
+        return img, st0, st1, int(nsel.value)
+
     def render(self, params):
         """Synchronous render to host; returns (image[rows, W, 3], Stats)."""
         rows = rows_in_shard(params)

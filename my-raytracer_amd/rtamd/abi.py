@@ -182,6 +182,8 @@ HIP_SYMBOLS = {
                                             C.POINTER(C.c_longlong), C.c_void_p]),
     "rt_adaptive_halo_rows": (C.c_int, [C.POINTER(RenderParams), C.POINTER(C.c_int), C.c_int]),
     "rt_render_to_host": (C.c_int, [C.c_void_p, C.POINTER(RenderParams), C.c_void_p, C.POINTER(Stats)]),
+    "rt_render_adaptive_to_host": (C.c_int, [C.c_void_p, C.POINTER(RenderParams), C.c_int, C.c_double, C.c_void_p,
+                                             C.POINTER(Stats), C.POINTER(Stats), C.POINTER(C.c_longlong)]),
     "rt_last_kernel_ms": (C.c_int, [C.c_void_p, C.POINTER(C.c_float)]),
     "rt_tile_shape": (C.c_int, [C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "rt_ipc_get_handle": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(C.c_ulonglong)]),

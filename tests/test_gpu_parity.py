@@ -596,6 +596,28 @@ def test_cli_renders(tmp_path):
     assert diff.max() <= 1 and (diff == 0).mean() >= 0.999, (diff.max(), (diff != 0).sum())
 
 
+def test_cli_adaptive_renders(tmp_path):
+    # rt_render --adaptive: the primary + adaptive pass of launch_compute_image_device through
+    # rt_render_adaptive_to_host -- the 8-bit image equals the library's fp32 result quantised the
+    # same way, and the selection count is the library's
+    out = tmp_path / "a.ppm"
+    r = subprocess.run([str(ROOT / "my-raytracer_amd/bin/rt_render"), "--scene", "office", "--width", "160",
+                        "--height", "90", "--adaptive", "--out", str(out)], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr
+    hs, dev, _ = Case.get("office")
+    p = hs.render_params(160, 90, 1)
+    p.out_format = rtamd.RT_OUT_RGB_F32
+    img, _, _, n = dev.render_adaptive_to_host(p)
+    assert f"re-rendered {n} pixels" in r.stdout
+    data = out.read_bytes()
+    head = b"P6\n160 90\n255\n"
+    assert data.startswith(head)
+    got = np.frombuffer(data[len(head):], np.uint8).reshape(90, 160, 3).astype(int)
+    want = np.floor(np.clip(img[::-1], 0, 1) * np.float32(255) + 0.5).astype(int)
+    assert np.abs(got - want).max() <= 1
+
+
 @pytest.mark.parametrize("kind,kw,w,h", [("office", {}, 192, 108), ("cornell", {}, 80, 60)])
 def test_adaptive_pass_matches_oracle(kind, kw, w, h):
     # adaptive_supersampling_device (mytracer_gpu.cu:162-229), subp 4, threshold 0.02.
@@ -671,6 +693,31 @@ def test_adaptive_end_to_end_and_full_frame_only():
     p.stripe_count, p.stripe_height = 2, 16
     with pytest.raises(rtamd.RtError):
         dev.render_adaptive(p)
+
+
+@pytest.mark.parametrize("fmt", ["f64", "f32"])
+def test_render_adaptive_to_host_equals_device_passes(fmt):
+    # rt_render_adaptive_to_host: the reference's launch_compute_image_device in one synchronous
+    # call (primary + adaptive pass + copy back), into pageable and page-locked host memory -- the
+    # same pixels, selection and ray counts as the two device-buffer passes
+    import torch
+
+    hs, dev, _ = Case.get("office")
+    p = rtamd.camera_orbit(hs.render_params(160, 90, 1), 0.03)
+    p.out_format = rtamd.RT_OUT_RGB_F64 if fmt == "f64" else rtamd.RT_OUT_RGB_F32
+    want, s0, s1, n = dev.render_adaptive(p)
+    page, t0, t1, m = dev.render_adaptive_to_host(p)
+    dt = torch.float64 if fmt == "f64" else torch.float32
+    pinned = torch.full((90, 160, 3), -1.0, dtype=dt).pin_memory()
+    pin, u0, u1, k = dev.render_adaptive_to_host(p, out=pinned.numpy())
+    for img in (page, pin):
+        assert np.array_equal(img, want)
+    assert n == m == k and n > 0
+    for a, b in ((s0, t0), (s1, t1), (s0, u0), (s1, u1)):
+        assert counts(a) == counts(b)
+    p.stripe_count, p.stripe_height = 2, 16
+    with pytest.raises(rtamd.RtError):
+        dev.render_adaptive_to_host(p)
 
 
 @pytest.mark.parametrize("n_lights", [rtamd.abi.RT_MAX_LIGHTS, 17, 64])
