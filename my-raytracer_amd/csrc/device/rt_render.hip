@@ -95,11 +95,13 @@ static_assert((kShortStack & kStackMask) == 0, "the stack ring must be a power o
 // extra shadow rays or its reflection ray, so a bounce costs one round, not 1 + lights.
 // PARKED (sample groups, spp > 1): the lane's sample is finished and its colour waits in the lane's
 // slot for its group's ordered sum (below); a parked lane is neither busy nor idle.
-// sample groups: pixels of a tile claimed in Morton order (RT_GROUP_ROW_ORDER: row order)
-#ifdef RT_GROUP_ROW_ORDER
-constexpr bool kGroupMorton = false;
+// a tile's pixels claimed in Morton order (RT_TILE_ROW_ORDER: row order): a partial refill's run of
+// items, or the 2-4 pixels of a wave's sample groups, is a compact block instead of a strip of rows
+// (r06t: configs 3 / 5 +0.4 %; r06u: office +0.5 %, config 4 +0.8 %)
+#ifdef RT_TILE_ROW_ORDER
+constexpr bool kTileMorton = false;
 #else
-constexpr bool kGroupMorton = true;
+constexpr bool kTileMorton = true;
 #endif
 enum : int { ST_FETCH = 0, ST_CLOSEST = 1, ST_SHADOW = 2, ST_DONE = 3, ST_PARKED = 4, ST_HSHADOW = 5, ST_HCLOSEST = 6 };
 constexpr uint32_t kTaskNone = 0xffffffffu;
@@ -969,13 +971,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
             frame = P.n_frames > 1 ? (int)P.div_tiles_x.div(rem) : 0;
             const int tx = (int)(rem - (uint32_t)frame * (uint32_t)P.tiles_x);
             int jx = j & (kTileW - 1), jy = j >> kTileWLog;
-#ifdef RT_MORTON_ALL
-            if (kTileW == 8) {
-#else
-            if (kGroupMorton && group_log && kTileW == 8) {
-#endif
-              // sample groups: the tile's pixels in Morton order, so the 2-4 pixels that share a
-              // wave form a 2x1 / 2x2 block instead of a strip of a row
+            if (kTileMorton && kTileW == 8) {   // (kTileMorton)
               jx = (j & 1) | ((j >> 1) & 2) | ((j >> 2) & 4);
               jy = ((j >> 1) & 1) | ((j >> 2) & 2) | ((j >> 3) & 4);
             }
