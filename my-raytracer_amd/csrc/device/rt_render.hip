@@ -63,7 +63,10 @@ namespace {
 
 constexpr int kBlock = 256;        // threads per persistent block
 constexpr int kGroups = 8;          // work heads (XCD groups)
-constexpr int kRefill = 16;         // refill a wave when this many lanes are idle (8 / 32: +-0.2 %)
+#ifndef RT_REFILL
+#define RT_REFILL 16
+#endif
+constexpr int kRefill = RT_REFILL;  // refill a wave when this many lanes are idle (8 / 32: +-0.2 %)
 constexpr int kCtrWords = 40;       // [8,16) stats (STATS variants), [16,40) diagnostics (31: guard)
 // Traversal stack: the top kShortStack entries live in an LDS ring (slot i & kStackMask),
 // deeper entries spill to a per-lane global array.  Bounds LDS per block independently
