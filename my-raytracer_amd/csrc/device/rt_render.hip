@@ -66,7 +66,7 @@ constexpr int kGroups = 8;          // work heads (XCD groups)
 #ifndef RT_REFILL
 #define RT_REFILL 16
 #endif
-constexpr int kRefill = RT_REFILL;  // refill a wave when this many lanes are idle (8 / 32: +-0.2 %)
+constexpr int kRefill = RT_REFILL;  // refill a wave when this many lanes are idle (8 / 32: -1.1 / -1.0 %, r06y)
 constexpr int kCtrWords = 40;       // [8,16) stats (STATS variants), [16,40) diagnostics (31: guard)
 // Traversal stack: the top kShortStack entries live in an LDS ring (slot i & kStackMask),
 // deeper entries spill to a per-lane global array.  Bounds LDS per block independently
