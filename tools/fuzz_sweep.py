@@ -11,7 +11,7 @@ usage: python tools/fuzz_sweep.py FIRST_SEED N_SEEDS OUT.json
        python tools/fuzz_sweep.py --deep FIRST_SEED N_SEEDS OUT.json
 --deep: generated deep scenes instead -- random-triangle soups of 2^15 .. 2^20 triangles (the
 16-entry stack ring and global spills from 2^18 records on) and cornell boxes of random detail,
-random depth 0-5, at 96 x 64 with 1-2 spp.
+random depth 0-5, at 96 x 64 with 1x1, 2x2 or 4x4 spp.
 """
 import json
 import sys
@@ -66,7 +66,7 @@ def deep(s0, n, out):
         gen = {"detail": 1 + seed % 6} if kind == "cornell" else {"n_triangles": sizes[seed % len(sizes)]}
         hs = rtamd.HostScene.generate(kind, seed=seed, max_depth=seed % 6, **gen)
         hs.prepare()
-        p = hs.render_params(96, 64, 1 + seed % 2)
+        p = hs.render_params(96, 64, (1, 2, 4)[seed % 3])   # 2x2 / 4x4: sample groups
         err, same, rays = check(hs, p, False, ("sbvh", "sah") if seed % 3 == 0 else ("sbvh",))
         ok = err <= TOL64 and same
         res = {"seed": seed, "scene": kind, **gen, "depth": seed % 6, "max_abs_err": err,
