@@ -98,6 +98,9 @@ def test_rank_shape_profiles_feed_n_gpu_lines():
             assert pmc is not None and pmc["read"] > 0 and pmc["write"] > 0, (n, fpl)
             assert b.pmc_valu_roof(dict(key, n_gpus=n), fpl, 0.1e-3) is not None, n
             assert b.pmc_wave_mix(dict(key, n_gpus=n), fpl) is not None, n
+            # the gather's shape (10 frames per launch) and the peer assembly's (20) each find the
+            # summary profiled at their own frames per launch
+            assert pmc["source"].endswith("_f20.json") == (fpl == 20.0), (n, fpl, pmc["source"])
 
 
 def _launch(args, env_extra=None, timeout=240):
