@@ -175,7 +175,7 @@ enum : int {
   CD_NODE_ITERS = 16, CD_NODE_LANES, CD_LEAF_ITERS, CD_LEAF_LANES, CD_TRAV_CYCLES, CD_SHADE_CYCLES,
   CD_FETCH_CYCLES, CD_OUTER_ITERS, CD_TRAV_ROUNDS, CD_TRAV_ROUND_LANES, CD_SPILLS, CD_NODE_LINES,
   CD_LEAF_LINES, CD_BIG_LEAF_TESTS, CD_NODE_LDS_ITERS, CD_GUARD = 31,   // CD_GUARD: a wave hit the iteration guard
-  CD_GNODE_UNIFORM = 32, CD_GNODE_DISTINCT, CD_LEAF_UNIFORM,
+  CD_GNODE_UNIFORM = 32, CD_GNODE_DISTINCT, CD_LEAF_UNIFORM, CD_ANYHIT_TRIS, CD_OWN_TRIS,
   CT_ORDER_JOBS = 39   // cost-ordered launches: order / zeroing jobs claimed by blocks that finished
 };
 // Watchdogs (never reached by a correct kernel): the persistent loop, and the wave-level
@@ -768,6 +768,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
   uint32_t pix_t0 = 0;      // start of the pixel (s_memrealtime; cost maps in time mode.  A pixel handed
                             // over by tail compaction restarts it at its adoption)
   int best = kNoHit;        // device record of the closest hit
+  int own_rec = -1;         // device record the bounce being shaded hit (its shadow rays start on it)
   int best_slot = kNoHit;   // its reference slot (tie-break key)
   double thit = DBL_MAX;
   bool shadow_hit = false;
@@ -780,6 +781,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
   unsigned long long d_node_it = 0, d_node_ln = 0, d_leaf_it = 0, d_leaf_ln = 0;
   unsigned long long d_trav = 0, d_shade = 0, d_fetch = 0, d_outer = 0, d_round_it = 0, d_round_ln = 0;
   unsigned long long d_spills = 0, d_node_lines = 0, d_leaf_lines = 0, d_big_leaf = 0, d_node_lds = 0, d_dummy = 0, d_gn_uni = 0, d_gn_dist = 0, d_leaf_uni = 0;
+  unsigned long long d_any_tris = 0, d_own_tris = 0;   // any-hit triangle tests; of those, the ray's own record
   unsigned long long w_start = STATS ? __builtin_amdgcn_s_memrealtime() : 0ull, w_refill = 0, w_pixels = 0;
   unsigned long long t_stamp = 0;
   // TL (round timeline, diagnostics): rounds recorded by this wave, the round's start stamp and
@@ -1071,6 +1073,9 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
         *R.o[0] = ro.x; *R.o[1] = ro.y; *R.o[2] = ro.z;
         *R.d[0] = rd.x; *R.d[1] = rd.y; *R.d[2] = rd.z;
       }
+      // the record this any-hit ray starts on (the owner's shading hit; helpers read their owner's)
+      int own = -1;
+      if (anyhit) own = (state == ST_SHADOW) ? own_rec : __shfl(own_rec, (int)(htask & 63u));
       best = kNoHit;
       best_slot = kNoHit;
       shadow_hit = false;
@@ -1209,6 +1214,10 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
               wave_distinct((uint32_t)(((unsigned long long)i * sizeof(GTri)) >> 7), d_leaf_lines, lane);
               const uint32_t i0 = __shfl(i, __ffsll((long long)wballot(1)) - 1);
               if (wballot(i != i0) == 0) wave_tick(d_leaf_uni, d_dummy, lane);
+            }
+            if (STATS && anyhit) {   // (r06zg: the own record is 14 % of the office's any-hit tests; skipping
+              d_any_tris++;          // it, unchecked, cost 3.7 %: DESIGN.md §11.12)
+              if ((int)rec == own) d_own_tris++;
             }
             const TriOps T = load_tri(P.tris, rec);
             const int slot = (int)(T.meta & kSlotMask);
@@ -1601,6 +1610,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
 #pragma unroll
             for (int k = 0; k < kSlotDoubles; ++k) lds_d[k * kBlock + threadIdx.x] = lds_d[k * kBlock + t];
             thit = *R.tlim;   // a closest-hit ray's distance (a shadow batch's owner does not read thit)
+            own_rec = -1;     // (not migrated: an adopted shadow batch tests every record)
             pix_t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
           }
           I &= ~wballot(take);
@@ -1712,6 +1722,7 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
           finish = true;
         } else {
           if (STATS) c_hits++;
+          own_rec = best;
           // hit attributes: mymesh.cpp:217-235 (texture :70-95)
           const D3 ro = d3(*R.o[0], *R.o[1], *R.o[2]);
           const D3 rd = d3(*R.d[0], *R.d[1], *R.d[2]);
@@ -1945,7 +1956,10 @@ __global__ void __launch_bounds__(kBlock, kWavesPerEU * 256 / kBlock) render_ker
     const unsigned long long g = wave_sum(d_spills), h = wave_sum(d_node_lines), q = wave_sum(d_leaf_lines);
     const unsigned long long r = wave_sum(d_big_leaf), t = wave_sum(d_node_lds);
     const unsigned long long gu = wave_sum(d_gn_uni), gd = wave_sum(d_gn_dist), lu = wave_sum(d_leaf_uni);
+    const unsigned long long at = wave_sum(d_any_tris), ot = wave_sum(d_own_tris);
     if (lane == 0) {
+      atomicAdd(&P.ctr[CD_ANYHIT_TRIS], at);
+      atomicAdd(&P.ctr[CD_OWN_TRIS], ot);
       atomicAdd(&P.ctr[CD_NODE_LDS_ITERS], t);
       atomicAdd(&P.ctr[CD_GNODE_UNIFORM], gu);
       atomicAdd(&P.ctr[CD_GNODE_DISTINCT], gd);

@@ -400,7 +400,8 @@ class DeviceScene:
         names = {16: "node_iters", 17: "node_lanes", 18: "leaf_iters", 19: "leaf_lanes", 20: "trav_cycles",
                  21: "shade_cycles", 22: "fetch_cycles", 23: "outer_iters", 24: "trav_rounds", 25: "trav_round_lanes",
                  26: "stack_spills", 27: "node_lines", 28: "leaf_lines", 29: "big_leaf_tests",
-                 30: "node_lds_iters", 32: "gnode_uniform_iters", 33: "gnode_distinct", 34: "leaf_uniform_iters"}
+                 30: "node_lds_iters", 32: "gnode_uniform_iters", 33: "gnode_distinct", 34: "leaf_uniform_iters",
+                 35: "anyhit_tri_tests", 36: "anyhit_own_record_tests"}
         return {v: int(buf[k]) for k, v in names.items()}
 
     def wave_log(self, max_waves=1 << 16):
