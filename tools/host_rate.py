@@ -1,7 +1,8 @@
 """Host-buffer call rate (dev tool, under gpurun): the reference's call pattern -- one synchronous
 frame per call, the image back in host memory (Raytracer::compute_image_cuda, mytracer.cpp:123-159)
 -- through rt_render_to_host into page-locked and into pageable memory, beside one-frame launches
-into a device buffer (launch + synchronise).  Office proxy 1080p fp32, consecutive orbit views;
+into a device buffer (launch + synchronise); and the reference's whole launch_compute_image_device
+(primary + adaptive pass + copy back) through rt_render_adaptive_to_host.  Office proxy 1080p fp32, consecutive orbit views;
 median ms per call over REPS calls.  RTAMD_HIP_LIB selects the library (A/B).
 
 usage: python tools/host_rate.py [REPS]
@@ -59,6 +60,13 @@ def host(buf_ptr):
     return f
 
 
+def host_adaptive(buf_ptr):   # the reference's whole call: primary + adaptive pass + copy back
+    def f(v):
+        rc = lib.rt_render_adaptive_to_host(dev._h, C.byref(v), 4, 0.02, C.c_void_p(buf_ptr), None, None, None)
+        assert rc == 0, rc
+    return f
+
+
 def d2h(v):   # the PCIe leg alone: a finished frame copied into page-locked memory
     pinned.copy_(d_out, non_blocking=True)
     torch.cuda.synchronize()
@@ -75,5 +83,7 @@ torch.cuda.synchronize()
 ref = d_out.cpu().numpy()
 res["pinned_equal"] = bool(np.array_equal(pinned.numpy(), ref))
 res["pageable_equal"] = bool(np.array_equal(pageable, ref))
-res.update({"d2h_copy_pinned_ms": timed(d2h), "frame_MB": round(W * H * 12 / 1e6, 2)})
+res.update({"d2h_copy_pinned_ms": timed(d2h), "frame_MB": round(W * H * 12 / 1e6, 2),
+            "adaptive_pinned_host_ms": timed(host_adaptive(pinned.data_ptr())),
+            "adaptive_pageable_host_ms": timed(host_adaptive(pageable.ctypes.data))})
 print(json.dumps(res), flush=True)
