@@ -85,7 +85,11 @@ constexpr int kStackMask = kShortStack - 1;
 // of a launch run in fewer, fuller waves.  A handed-over lane's registers travel through the
 // donor thread's LDS stack entries (free between traversals): kMigWords words (packed; the
 // closest-hit distance and the hit attributes travel in the LDS slot, copied with it).
-constexpr int kDonateMax = 24;   // (0 = tail compaction off: -2.8 % batched, -1.4 % one frame)
+#ifndef RT_DONATE_MAX
+#define RT_DONATE_MAX 24
+#endif
+constexpr int kDonateMax = RT_DONATE_MAX;   // (0 = tail compaction off: -2.8 % batched, -1.4 % one frame;
+                                            //  16 / 32 / 40: within noise, r06zr/r06zs)
 constexpr int kMigWords = 8;
 static_assert(kMigWords <= kShortStack, "migration words travel in the stack ring entries");
 constexpr int kPoolBytes = 64;   // LDS: live-wave count, one 64-bit lane mask per wave of the block, exhausted heads
